@@ -1,0 +1,233 @@
+"""BA3C train-step throughput on MI355X (BASELINE.json metric).
+
+One step = forward + A3C loss + backward + per-tensor clip + (RCCL gradient mean for N>1) +
+Adam, on a synthetic 84x84x4 uint8 frame batch already resident in HBM.  Default workload:
+configs[2]/[3] — B=2048 per GPU, fc_neurons=512, fc_splits=1, A=4 (Breakout), Adam with the
+README's best hyper-parameters.  The B=32 / F=128 / S=4 parity configuration (configs[1]) is
+timed beside it.  Rank 0 prints ONE JSON line.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N ... bench.py --gpus N   (one process per GPU, RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-ba3c_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "BA3C train-step samples/sec, 84x84x4 frames, batch 32 & 2048, at 1/2/4/8 GPUs"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (spec)
+
+# algorithmic MAC per sample of each layer's forward product (real C input channels;
+# SURVEY.md §8d), backward kernels of a layer do the same algorithmic work
+def layer_macs(C, F):
+    return {"conv0": 6400 * 32 * 25 * C, "conv1": 1296 * 32 * 800, "conv2": 196 * 64 * 800,
+            "conv3": 25 * 64 * 576, "fc1": 1600 * F}
+
+
+KERNEL_LAYER = {"conv0_fwd": "conv0", "conv1_fwd": "conv1", "conv2_fwd": "conv2",
+                "conv3_fwd": "conv3", "fc1_fwd": "fc1", "conv1_dgrad": "conv1",
+                "conv2_dgrad": "conv2", "conv3_dgrad": "conv3", "fc1_dgrad": "fc1",
+                "conv0_wgrad": "conv0", "conv1_wgrad": "conv1", "conv2_wgrad": "conv2",
+                "conv3_wgrad": "conv3", "fc1_wgrad": "fc1"}
+
+
+def train_step_flops(B, C, F, A=4):
+    """fwd + wgrad(all) + dgrad(all but conv0), real input channels."""
+    m = layer_macs(C, F)
+    fwd = sum(m.values())
+    return 2.0 * (fwd + fwd + (fwd - m["conv0"])) * B
+
+
+def build_trainer(B, F, S, A, world, seed):
+    from ba3c_amd.model import Model
+    from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
+    from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
+    from oracle.ba3c_oracle import init_params  # weight initialiser only (numpy RNG)
+
+    model = Model(num_actions=A, channels=1, fc_neurons=F, fc_splits=S, batch_size=B, max_batch=B)
+    model.engine.load_params(init_params(F, S, A, seed=0, dtype=np.float32))
+    opt = AdamOptimizer(1e-3, beta1=0.8, beta2=0.75, epsilon=1e-8)   # README.md:35
+    if world > 1:
+        opt = SyncReplicasOptimizer(opt, replicas_to_aggregate=world, total_num_replicas=world)
+    tr = Ba3cTrainer(TrainConfig(model=model, optimizer=opt))
+    g = torch.Generator(device="cuda").manual_seed(1000 + seed)
+    state = torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device="cuda", generator=g)
+    action = torch.randint(0, A, (B,), dtype=torch.int64, device="cuda", generator=g)
+    R = torch.randn(B, dtype=torch.float32, device="cuda", generator=g)
+    return tr, (state, action, R)
+
+
+def sync_all(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def time_steps(tr, batch, steps, warmup, world, probe=None):
+    for _ in range(warmup):
+        tr.train_step(*batch)
+    sync_all(world)
+    if probe is not None:
+        tr.engine.probe_enable(probe)   # bracket the dominant kernel over the timed steps only
+    t0 = time.perf_counter()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(steps):
+        tr.train_step(*batch)
+    ev1.record()
+    sync_all(world)
+    wall = time.perf_counter() - t0
+    gpu_s = ev0.elapsed_time(ev1) / 1000.0
+    el = torch.tensor([max(wall, gpu_s)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item())
+
+
+def find_dominant_kernel(tr, batch):
+    from ba3c_amd._lib import KERNEL_IDS
+    eng = tr.engine
+    best, best_ms, per = None, -1.0, {}
+    for name in KERNEL_IDS:
+        eng.probe_enable(name)
+        tr.train_step(*batch)
+        ms, n = eng.probe_read()
+        per[name] = ms
+        if ms > best_ms:
+            best, best_ms = name, ms
+    eng.probe_enable(None)
+    return best, per
+
+
+def cpu_baseline(F, S, A, seconds=12.0):
+    """The oracle (numpy float32 restatement of the TF graph incl. 16-channel padding, TF clip,
+    TF Adam) timed on this host on a bounded sample: steps of B=16 frames until ~`seconds`."""
+    from oracle import ba3c_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    rs = np.random.RandomState(0)
+    B = 16
+    params = O.init_params(F, S, A, seed=0, dtype=np.float32)
+    slots = O.init_slots(params, "adam", 0.8, 0.75)
+    cfg = {"fc_neurons": F, "fc_splits": S}
+    state = rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)
+    action = rs.randint(0, A, size=B).astype(np.int64)
+    R = rs.normal(size=B).astype(np.float32)
+    O.train_step(params, slots, 1, [(state, action, R)], cfg, lr=1e-3, beta1=0.8, beta2=0.75)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        params, slots, _, _ = O.train_step(params, slots, 1, [(state, action, R)], cfg, lr=1e-3,
+                                           beta1=0.8, beta2=0.75)
+        n += 1
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(n * B / dt, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": "%d numpy-fp32 oracle train steps of B=%d (F=%d, S=%d) in %.1f s on %s"
+                      % (n, B, F, S, dt, cpu)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--fc_neurons", type=int, default=512)
+    ap.add_argument("--fc_splits", type=int, default=1)
+    ap.add_argument("--num_actions", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-b32", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d (launch N>1 with torch.distributed.run)"
+                         % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    B, F, S, A = args.batch, args.fc_neurons, args.fc_splits, args.num_actions
+    tr, batch = build_trainer(B, F, S, A, world, seed=rank)
+    for _ in range(2):
+        tr.train_step(*batch)
+    sync_all(world)
+    dom, per_kernel = find_dominant_kernel(tr, batch)
+    sync_all(world)
+
+    elapsed = time_steps(tr, batch, args.steps, args.warmup, world, probe=dom)
+    probe_ms, launches = tr.engine.probe_read()
+    tr.engine.probe_enable(None)
+
+    value = world * B * args.steps / elapsed
+    ms_step = elapsed / args.steps * 1000.0
+    C = 4
+    macs = layer_macs(C, F)
+    dom_flops = 2.0 * macs[KERNEL_LAYER[dom]] * B if dom in KERNEL_LAYER else None
+    avg_ms = probe_ms / max(launches, 1)
+    roof = None
+    if dom_flops:
+        ach = dom_flops / (avg_ms / 1000.0) / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "avg_launch_ms": round(avg_ms, 4), "launches": launches}
+    step_tflops = train_step_flops(B, C, F, A) / (ms_step / 1000.0) / 1e12
+
+    out = {"metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic uint8 84x84x4 frames, random actions/returns, weights from the "
+                   "reference initialisers (seed 0); resident in HBM",
+           "config": {"workload": "configs[2]/[3]: BA3C train step (fwd+bwd+clip+%sAdam) "
+                                  "B=%d/GPU, fc_neurons=%d, fc_splits=%d, A=%d"
+                                  % ("RCCL mean+" if world > 1 else "", B, F, S, A),
+                      "global_batch": world * B, "per_gpu_batch": B, "fc_neurons": F,
+                      "fc_splits": S, "num_actions": A, "parallelism": "dp%d" % world},
+           "step_tflops_algorithmic": round(step_tflops, 2),
+           "step_mfma_frac": round(step_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+           "roofline": roof,
+           "kernel_ms_one_step": {k: round(v, 4) for k, v in per_kernel.items()}}
+
+    if not args.no_b32:
+        del tr
+        tr32, b32 = build_trainer(32, 128, 4, A, world, seed=rank)
+        el32 = time_steps(tr32, b32, max(args.steps, 50), 10, world)
+        n32 = max(args.steps, 50)
+        out["b32"] = {"config": "configs[1]: B=32/GPU, fc_neurons=128, fc_splits=4",
+                      "value": round(world * 32 * n32 / el32, 1), "unit": "samples/s",
+                      "ms_per_step": round(el32 / n32 * 1000.0, 4)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(F, S, A, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

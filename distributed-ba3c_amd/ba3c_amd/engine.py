@@ -1,0 +1,188 @@
+"""Ba3cEngine — owns the flat parameter / gradient / optimizer-slot buffers (PyTorch-ROCm
+device memory) and drives libba3c.so's HIP kernels on the current HIP stream.
+
+This is the MI355X replacement of everything the reference's `sess.run(TfDictOp.op)`
+executed per step (tensorpack_cpu/tensorpack/train/trainer.py:282): forward, loss,
+autodiff, gradient processor and optimizer apply, plus the predictor's
+`sess.run(['towerp0/logitsT','towerp0/pred_value'])` (predict/base.py:80-92).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_F32 = np.float32
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Ba3cEngine(object):
+    """One network instance on one GPU.
+
+    Parameters mirror the reference flag surface: `channels` = FRAME_HISTORY*--channels
+    (train.py:95), `fc_neurons` (--fc_neurons), `fc_splits` (--fc_splits),
+    `replace_with_conv` (default True; False = --use_normal_fc with `ps` splits).
+    """
+
+    def __init__(self, num_actions=4, channels=4, fc_neurons=512, fc_splits=1,
+                 replace_with_conv=True, ps=1, max_batch=2048, device=None):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.Ba3cLibraryError("Ba3cEngine needs a ROCm GPU (torch.cuda unavailable)")
+        self.device = torch.device(device or "cuda")
+        self.cfg = dict(num_actions=num_actions, channels=channels, fc_neurons=fc_neurons,
+                        fc_splits=fc_splits, replace_with_conv=replace_with_conv, ps=ps)
+        c = _lib.Ba3cConfig(max_batch, channels, fc_neurons, fc_splits, num_actions,
+                            1 if replace_with_conv else 0, ps)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.ba3c_create(ctypes.byref(c), ctypes.byref(h)))
+        self.h = h
+        self.max_batch = max_batch
+        self.num_actions = num_actions
+        self.channels = channels
+        self.layout = []
+        for i in range(self.lib.ba3c_num_tensors(h)):
+            name = ctypes.c_char_p()
+            off, numel = ctypes.c_int64(), ctypes.c_int64()
+            shape = (ctypes.c_int32 * 4)()
+            nd = ctypes.c_int32()
+            _lib.check(self.lib.ba3c_tensor_info(h, i, ctypes.byref(name), ctypes.byref(off),
+                                                 ctypes.byref(numel), shape, ctypes.byref(nd)))
+            self.layout.append((name.value.decode(), off.value, numel.value,
+                                tuple(shape[k] for k in range(nd.value))))
+        self.flat_size = int(self.lib.ba3c_flat_size(h))
+        with torch.cuda.device(self.device):
+            z = lambda: torch.zeros(self.flat_size, dtype=torch.float32, device=self.device)
+            self.params = z()
+            self.grads = z()
+            self.ws_train = None
+            self.ws_fwd = None
+            self.scalars = torch.zeros(8, dtype=torch.float64, device=self.device)
+
+    # -- parameters -------------------------------------------------------------------
+    @property
+    def tensor_names(self):
+        return [n for n, _, _, _ in self.layout]
+
+    def view(self, flat, name):
+        for n, off, numel, shape in self.layout:
+            if n == name:
+                return flat[off:off + numel].view(shape)
+        raise KeyError(name)
+
+    def load_params(self, params):
+        """Copy a {name: ndarray} dict (TF layout, e.g. oracle.init_params) into the flat buffer."""
+        for n, off, numel, shape in self.layout:
+            v = np.ascontiguousarray(params[n], dtype=_F32)
+            assert v.shape == shape, (n, v.shape, shape)
+            self.params[off:off + numel].copy_(torch.from_numpy(v.reshape(-1)))
+
+    def state_dict(self, flat=None):
+        flat = self.params if flat is None else flat
+        host = flat.detach().cpu().numpy()
+        return {n: host[off:off + numel].reshape(shape).copy() for n, off, numel, shape in self.layout}
+
+    def zeros_like_flat(self, fill=0.0):
+        return torch.full((self.flat_size,), fill, dtype=torch.float32, device=self.device)
+
+    # -- workspaces ---------------------------------------------------------------------
+    def _workspace(self, train):
+        if train:
+            if self.ws_train is None:
+                n = self.lib.ba3c_workspace_size(self.h, self.max_batch, 1)
+                self.ws_train = torch.empty(n, dtype=torch.uint8, device=self.device)
+            return self.ws_train
+        if self.ws_fwd is None:
+            n = self.lib.ba3c_workspace_size(self.h, self.max_batch, 0)
+            self.ws_fwd = torch.empty(n, dtype=torch.uint8, device=self.device)
+        return self.ws_fwd
+
+    def _check_state(self, state):
+        assert state.dtype == torch.uint8 and state.is_cuda and state.is_contiguous(), \
+            "state must be a contiguous uint8 device tensor [B,84,84,C]"
+        assert state.dim() == 4 and tuple(state.shape[1:]) == (84, 84, self.channels), state.shape
+        B = state.shape[0]
+        assert 1 <= B <= self.max_batch, "batch %d outside [1, %d]" % (B, self.max_batch)
+        return B
+
+    # -- hot path -------------------------------------------------------------------------
+    def forward(self, state, explore_factor=1.0, params=None, out=None):
+        """Predictor forward: returns (probs 'logits', probsT 'logitsT', value 'pred_value')."""
+        B = self._check_state(state)
+        A = self.num_actions
+        if out is None:
+            out = (torch.empty(B, A, dtype=torch.float32, device=self.device),
+                   torch.empty(B, A, dtype=torch.float32, device=self.device),
+                   torch.empty(B, dtype=torch.float32, device=self.device))
+        params = self.params if params is None else params
+        _lib.check(self.lib.ba3c_forward(self.h, _stream(), _ptr(params), _ptr(state), B,
+                                         float(explore_factor), _ptr(self._workspace(False)),
+                                         _ptr(out[0]), _ptr(out[1]), _ptr(out[2])))
+        return out
+
+    def train_grads(self, state, action, futurereward, entropy_beta=0.01, grads=None):
+        """Forward + loss + backward; raw gradients into `grads` (default self.grads).
+        Returns the device float64 scalars tensor (order: _lib.SCALAR_NAMES)."""
+        B = self._check_state(state)
+        assert action.dtype == torch.int64 and action.shape == (B,) and action.is_cuda
+        assert futurereward.dtype == torch.float32 and futurereward.shape == (B,)
+        grads = self.grads if grads is None else grads
+        _lib.check(self.lib.ba3c_train_grads(self.h, _stream(), _ptr(self.params), _ptr(state),
+                                             _ptr(action.contiguous()),
+                                             _ptr(futurereward.contiguous()), B,
+                                             float(entropy_beta), _ptr(self._workspace(True)),
+                                             _ptr(grads), _ptr(self.scalars)))
+        return self.scalars
+
+    def clip_grads(self, grads=None):
+        """tf.clip_by_average_norm(g, 0.1) per tensor, in place (train.py:329-330)."""
+        grads = self.grads if grads is None else grads
+        _lib.check(self.lib.ba3c_clip_grads(self.h, _stream(), _ptr(grads),
+                                            _ptr(self._workspace(True))))
+
+    def apply_update(self, opt, slot0, slot1, hp, grad_scale=1.0, fuse_clip=False, grads=None):
+        grads = self.grads if grads is None else grads
+        p = _lib.Ba3cOptParams(**hp)
+        _lib.check(self.lib.ba3c_apply_update(self.h, _stream(), _lib.OPT_IDS[opt],
+                                              _ptr(self.params), _ptr(grads), _ptr(slot0),
+                                              _ptr(slot1), ctypes.byref(p), float(grad_scale),
+                                              1 if fuse_clip else 0,
+                                              _ptr(self._workspace(True))))
+
+    def sample(self, probs, u, actions=None, flag=None):
+        """numpy RandomState.choice(A, p) given the uniform draws u (float64 device tensor)."""
+        B, A = probs.shape
+        assert u.dtype == torch.float64 and u.shape == (B,)
+        if actions is None:
+            actions = torch.empty(B, dtype=torch.int64, device=probs.device)
+        if flag is None:
+            flag = torch.zeros(1, dtype=torch.int32, device=probs.device)
+        _lib.check(self.lib.ba3c_sample(_stream(), _ptr(probs.contiguous()), _ptr(u), B, A,
+                                        _ptr(actions), _ptr(flag)))
+        return actions, flag
+
+    # -- timing probe -------------------------------------------------------------------
+    def probe_enable(self, kernel):
+        kid = -1 if kernel is None else _lib.KERNEL_IDS[kernel]
+        _lib.check(self.lib.ba3c_probe_enable(self.h, kid))
+
+    def probe_read(self):
+        ms, n = ctypes.c_double(), ctypes.c_int32()
+        _lib.check(self.lib.ba3c_probe_read(self.h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                self.lib.ba3c_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass

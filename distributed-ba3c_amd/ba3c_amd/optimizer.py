@@ -1,0 +1,192 @@
+"""TF-1.2 optimizers over the flat buffers (train.py:582-606) and SyncReplicasOptimizer.
+
+Slot initial values, the float32 beta-power variables and the scalar arithmetic follow the
+TF-1.2 CPU functors.  Every apply is ONE fused HIP kernel over
+the flat parameter buffer (`ba3c_apply_update`), optionally with clip_by_average_norm fused
+in (single replica).  SyncReplicasOptimizer replaces the parameter-server accumulators with
+an RCCL all-reduce of the flat clipped-gradient buffer (torch.distributed 'nccl' == RCCL).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+_f = np.float32
+
+
+class Optimizer(object):
+    opt_id = None
+    n_slots = 0
+
+    def __init__(self, learning_rate):
+        self.learning_rate = float(learning_rate)   # non-trainable 'learning_rate' var (train.py:536)
+        self.slots = None
+
+    def _init_slots(self, engine):
+        raise NotImplementedError
+
+    def _hparams(self):
+        return dict(lr=self.learning_rate, beta1=0.0, beta2=0.0, epsilon=0.0, beta1_power=0.5,
+                    beta2_power=0.5, decay=0.0, momentum=0.0, rho=0.0)
+
+    def _after_apply(self):
+        pass
+
+    def apply_gradients(self, engine, grad_scale=1.0, fuse_clip=False, grads=None):
+        """optimizer.apply_gradients(grads) (train/multigpu.py:194) over engine.grads."""
+        if self.slots is None:
+            self.slots = self._init_slots(engine)
+        s0 = self.slots[0] if len(self.slots) > 0 else None
+        s1 = self.slots[1] if len(self.slots) > 1 else None
+        engine.apply_update(self.opt_id, s0, s1, self._hparams(), grad_scale=grad_scale,
+                            fuse_clip=fuse_clip, grads=grads)
+        self._after_apply()
+
+    def slot_dict(self, engine, i):
+        return engine.state_dict(self.slots[i])
+
+
+class AdamOptimizer(Optimizer):
+    """tf.train.AdamOptimizer(lr, beta1, beta2, epsilon) — m, v zero-initialised; beta powers
+    are float32 variables initialised to beta1/beta2 and multiplied after each apply."""
+    opt_id = "adam"
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8):
+        super(AdamOptimizer, self).__init__(learning_rate)
+        self.beta1, self.beta2, self.epsilon = float(beta1), float(beta2), float(epsilon)
+        self.beta1_power = _f(beta1)
+        self.beta2_power = _f(beta2)
+
+    def _init_slots(self, engine):
+        return [engine.zeros_like_flat(), engine.zeros_like_flat()]
+
+    def _hparams(self):
+        h = super(AdamOptimizer, self)._hparams()
+        h.update(beta1=self.beta1, beta2=self.beta2, epsilon=self.epsilon,
+                 beta1_power=float(self.beta1_power), beta2_power=float(self.beta2_power))
+        return h
+
+    def _after_apply(self):
+        self.beta1_power = _f(self.beta1_power * _f(self.beta1))
+        self.beta2_power = _f(self.beta2_power * _f(self.beta2))
+
+
+class RMSPropOptimizer(Optimizer):
+    """tf.train.RMSPropOptimizer(lr) with TF-1.2 defaults; 'rms' slot initialised to ONES."""
+    opt_id = "rms"
+
+    def __init__(self, learning_rate, decay=0.9, momentum=0.0, epsilon=1e-10):
+        super(RMSPropOptimizer, self).__init__(learning_rate)
+        self.decay, self.momentum, self.epsilon = float(decay), float(momentum), float(epsilon)
+
+    def _init_slots(self, engine):
+        return [engine.zeros_like_flat(1.0), engine.zeros_like_flat()]
+
+    def _hparams(self):
+        h = super(RMSPropOptimizer, self)._hparams()
+        h.update(decay=self.decay, momentum=self.momentum, epsilon=self.epsilon)
+        return h
+
+
+class GradientDescentOptimizer(Optimizer):
+    opt_id = "gd"
+
+    def _init_slots(self, engine):
+        return []
+
+
+class MomentumOptimizer(Optimizer):
+    opt_id = "momentum"
+
+    def __init__(self, learning_rate, momentum=0.9):
+        super(MomentumOptimizer, self).__init__(learning_rate)
+        self.momentum = float(momentum)
+
+    def _init_slots(self, engine):
+        return [engine.zeros_like_flat()]
+
+    def _hparams(self):
+        h = super(MomentumOptimizer, self)._hparams()
+        h.update(momentum=self.momentum)
+        return h
+
+
+class AdagradOptimizer(Optimizer):
+    opt_id = "adagrad"
+
+    def __init__(self, learning_rate, initial_accumulator_value=0.1):
+        super(AdagradOptimizer, self).__init__(learning_rate)
+        self.init_acc = float(initial_accumulator_value)
+
+    def _init_slots(self, engine):
+        return [engine.zeros_like_flat(self.init_acc)]
+
+
+class AdadeltaOptimizer(Optimizer):
+    opt_id = "adadelta"
+
+    def __init__(self, learning_rate=0.001, rho=0.95, epsilon=1e-8):
+        super(AdadeltaOptimizer, self).__init__(learning_rate)
+        self.rho, self.epsilon = float(rho), float(epsilon)
+
+    def _init_slots(self, engine):
+        return [engine.zeros_like_flat(), engine.zeros_like_flat()]
+
+    def _hparams(self):
+        h = super(AdadeltaOptimizer, self)._hparams()
+        h.update(rho=self.rho, epsilon=self.epsilon)
+        return h
+
+
+def make_optimizer(name, lr, beta1=0.9, beta2=0.999, epsilon=1e-8):
+    """The `-o` switch of run_job.py / get_config (train.py:583-597)."""
+    if name == "adam":
+        return AdamOptimizer(lr, beta1=beta1, beta2=beta2, epsilon=epsilon)
+    if name == "gd":
+        return GradientDescentOptimizer(lr)
+    if name == "adagrad":
+        return AdagradOptimizer(lr)
+    if name == "adadelta":
+        return AdadeltaOptimizer(lr, epsilon=1e-3)
+    if name == "momentum":
+        return MomentumOptimizer(lr, momentum=0.9)
+    if name == "rms":
+        return RMSPropOptimizer(lr)
+    raise ValueError("unknown optimizer %r" % name)
+
+
+class SyncReplicasOptimizer(object):
+    """tf.train.SyncReplicasOptimizer(opt, replicas_to_aggregate, total_num_replicas)
+    (train.py:598-606) on one node: every rank clips its own gradients, the flat buffer is
+    summed over RCCL (one all-reduce of 1.3-3.8 MB), and every rank applies the same update
+    with grad_scale = 1/N, so replicas stay bit-identical.  Backup workers / stale-gradient
+    dropping (num_grad < n_workers) have no synchronous single-node equivalent: the
+    aggregation is always over all `total_num_replicas` ranks (documented deviation)."""
+
+    def __init__(self, opt, replicas_to_aggregate=None, total_num_replicas=None, group=None):
+        self._opt = opt
+        self.group = group
+        world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.total_num_replicas = total_num_replicas or world
+        self.replicas_to_aggregate = replicas_to_aggregate or self.total_num_replicas
+        if self.total_num_replicas != world or self.replicas_to_aggregate != world:
+            raise ValueError("synchronous all-reduce aggregates exactly world_size=%d replicas "
+                             "(got replicas_to_aggregate=%s, total_num_replicas=%s)"
+                             % (world, replicas_to_aggregate, total_num_replicas))
+        self.world = world
+
+    @property
+    def learning_rate(self):
+        return self._opt.learning_rate
+
+    @learning_rate.setter
+    def learning_rate(self, v):
+        self._opt.learning_rate = v
+
+    def aggregate(self, engine):
+        """Per-replica clip (multigpu.py:157) then the RCCL sum of the clipped buffer."""
+        engine.clip_grads()
+        if self.world > 1:
+            dist.all_reduce(engine.grads, op=dist.ReduceOp.SUM, group=self.group)
+
+    def apply_gradients(self, engine):
+        self._opt.apply_gradients(engine, grad_scale=1.0 / self.world, fuse_clip=False)

@@ -1,0 +1,115 @@
+"""Predictor path: OnlinePredictor (predict/base.py:72-92) and the MultiThreadAsyncPredictor
+(predict/concurrency.py:82-219), re-designed as ONE large-batch GPU forward.
+
+The reference answers each simulator state with a <=16-state micro-batch on 3 CPU threads;
+here queued states are concatenated and forwarded in a single `ba3c_forward` launch chain on
+a dedicated HIP stream (so it overlaps the learner's stream), and actions are sampled on the
+GPU with numpy-exact semantics from host-drawn MT19937 uniforms (train.py:382).
+"""
+import queue
+import threading
+
+import numpy as np
+import torch
+
+
+class OnlinePredictor(object):
+    """f([states]) -> [logitsT, pred_value, global_step, True] (predict/base.py:80-92);
+    on failure returns dummy outputs and the False flag like the reference (:86-91)."""
+
+    def __init__(self, model, input_names=("state",), output_names=("logitsT", "pred_value"),
+                 stream=None):
+        self.model = model
+        self.engine = model.engine
+        self.input_names = list(input_names)
+        self.output_names = list(output_names)
+        self.stream = stream
+        self.global_step = 0
+
+    def _forward(self, states):
+        eng = self.engine
+        if isinstance(states, np.ndarray):
+            states = torch.from_numpy(np.ascontiguousarray(states, dtype=np.uint8))
+        states = states.to(eng.device, non_blocking=True).contiguous()
+        probs, probsT, value = eng.forward(states, explore_factor=self.model.explore_factor)
+        outs = {"logits": probs, "logitsT": probsT, "pred_value": value}
+        return [outs[n] for n in self.output_names]
+
+    def __call__(self, dp):
+        states = dp[0]
+        try:
+            if self.stream is not None:
+                with torch.cuda.stream(self.stream):
+                    outs = self._forward(states)
+            else:
+                outs = self._forward(states)
+            return outs + [self.global_step, True]
+        except Exception:
+            n = len(states)
+            return [np.zeros((n, self.engine.num_actions), np.float32), np.zeros(n, np.float32),
+                    0, False]
+
+
+class MultiThreadAsyncPredictor(object):
+    """Queue of single-state tasks served in large batches (concurrency.py:172-219).
+
+    put_task([state], callback) enqueues; a worker thread drains up to `batch_size` tasks,
+    runs one GPU forward + GPU sampling, and calls each callback with
+    [probs_i, value_i, global_step, True, action_i].  `rs` is the numpy RandomState whose
+    uniform stream np.random.choice would consume (one double per state, in order)."""
+
+    def __init__(self, predictor, batch_size=8192, rs=None):
+        self.predictor = predictor
+        self.batch_size = batch_size
+        self.rs = rs if rs is not None else np.random.RandomState(0)
+        self.tasks = queue.Queue()
+        self._stop = threading.Event()
+        self._thread = None
+
+    def put_task(self, dp, callback=None):
+        self.tasks.put((dp, callback))
+
+    def run(self):
+        self._thread = threading.Thread(target=self._loop, daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join()
+
+    def _fetch_batch(self):
+        first = self.tasks.get(timeout=0.1)
+        batch = [first]
+        while len(batch) < self.batch_size:
+            try:
+                batch.append(self.tasks.get_nowait())
+            except queue.Empty:
+                break
+        return batch
+
+    def predict_batch(self, states):
+        """One forward of [b,84,84,C] states + sampling; returns host (probs, values, actions)."""
+        eng = self.predictor.engine
+        probs, value = self.predictor([states])[:2]
+        u = torch.from_numpy(np.array([self.rs.random_sample() for _ in range(len(states))],
+                                      dtype=np.float64)).to(eng.device)
+        actions, flag = eng.sample(probs, u)
+        f = int(flag.item())
+        if f & 1:
+            raise AssertionError("non-finite action distribution (train.py:381)")
+        if f & (2 | 4):
+            raise ValueError("probabilities do not sum to 1 / are negative")
+        return probs.cpu().numpy(), value.cpu().numpy(), actions.cpu().numpy()
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                batch = self._fetch_batch()
+            except queue.Empty:
+                continue
+            states = np.stack([np.asarray(dp[0]) for dp, _ in batch])
+            probs, values, actions = self.predict_batch(states)
+            for i, (_, cb) in enumerate(batch):
+                if cb is not None:
+                    cb([probs[i], values[i], self.predictor.global_step, True, int(actions[i])])

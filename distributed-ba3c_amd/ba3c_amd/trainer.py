@@ -1,0 +1,84 @@
+"""Learner step driver: QueueInputTrainer.run_step / AsyncMultiGPUTrainer.run_step
+(train/trainer.py:244-299, train/multigpu.py:131-324) re-designed for one process per GPU.
+
+One `run_step(batch)` = forward + A3C loss + backward (one HIP launch chain), the model's
+gradient processors (fused clip), the synchronous RCCL gradient mean when
+SyncReplicasOptimizer is used, and one fused optimizer apply; it returns the TfDictOp
+dictionary of the reference (multigpu.py:193-205).
+"""
+import time
+
+import numpy as np
+import torch
+
+from .model_desc import ClipByAverageNorm, MapGradient
+from .optimizer import SyncReplicasOptimizer
+
+
+class TrainConfig(object):
+    """train/config.py:15-84 (the fields this path uses)."""
+
+    def __init__(self, model, optimizer, dataset=None, step_per_epoch=250, max_epoch=1000,
+                 callbacks=None, extra_arg=None):
+        self.model = model
+        self.optimizer = optimizer
+        self.dataset = dataset
+        self.step_per_epoch = step_per_epoch
+        self.max_epoch = max_epoch
+        self.callbacks = callbacks or []
+        self.extra_arg = extra_arg or {}
+
+
+class Ba3cTrainer(object):
+    def __init__(self, config):
+        self.config = config
+        self.model = config.model
+        self.engine = config.model.engine
+        self.optimizer = config.optimizer
+        self.global_step = 0
+        self.step_ms = []
+        procs = self.model.get_gradient_processor()
+        self._fused_clip = (len(procs) == 1 and isinstance(procs[0], MapGradient)
+                            and isinstance(procs[0].func, ClipByAverageNorm)
+                            and procs[0].regex == ".*$")
+        self._procs = procs
+
+    def process_grads(self):
+        for p in self._procs:
+            p.process(self.engine)
+
+    def train_step(self, state, action, futurereward):
+        """Device-side step with no host synchronisation (used by bench.py)."""
+        self.model.build_graph([state, action, futurereward])
+        opt = self.optimizer
+        if isinstance(opt, SyncReplicasOptimizer):
+            if self._fused_clip:
+                opt.aggregate(self.engine)
+            else:
+                self.process_grads()
+                if opt.world > 1:
+                    torch.distributed.all_reduce(self.engine.grads)
+            opt.apply_gradients(self.engine)
+        elif self._fused_clip:
+            opt.apply_gradients(self.engine, fuse_clip=True)
+        else:
+            self.process_grads()
+            opt.apply_gradients(self.engine)
+        self.global_step += 1
+
+    def run_step(self, batch):
+        """batch = [state, action, futurereward, ts, init_R, isOver] (train.py:432) as numpy or
+        tensors; returns the TfDictOp dict incl. global_step and dp_per_s (multigpu.py:307-313)."""
+        t0 = time.time()
+        dev = self.engine.device
+        state = torch.as_tensor(np.asarray(batch[0], dtype=np.uint8)).to(dev)
+        action = torch.as_tensor(np.asarray(batch[1], dtype=np.int64)).to(dev)
+        R = torch.as_tensor(np.asarray(batch[2], dtype=np.float32)).to(dev)
+        self.train_step(state, action, R)
+        out = self.model.scalars_dict()      # synchronises the stream
+        if len(batch) > 3 and batch[3] is not None:
+            out["delay"] = float(np.mean(self.global_step - np.asarray(batch[3], np.float64)))
+        out["global_step"] = self.global_step
+        self.step_ms.append((time.time() - t0) * 1000.0)
+        out["dp_per_s"] = 1000.0 / np.mean(self.step_ms[-20:]) * state.shape[0]
+        return out

@@ -1,0 +1,625 @@
+// ba3c_capi.hip — C ABI (include/ba3c.h) and step orchestration of libba3c.so.
+//
+// One call of ba3c_train_grads runs, on the caller's stream, the whole tower of
+// train.py:164-327 plus its TF autodiff (train/multigpu.py:85-86):
+//   conv0..conv3 forward (ReLU, max-pool + argmax codes fused), fc1, heads+softmax+loss,
+//   then backward: head/fc1/conv weight gradients (split-K MFMA + deterministic reduce)
+//   and input gradients (MFMA dgrad with MaxPoolGrad/ReluGrad fused into the loaders).
+// No device allocation and no synchronisation happen inside any entry point.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ba3c.h"
+#include "ba3c_problems.h"
+#include "ba3c_small.h"
+
+using namespace ba3c;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return fail(BA3C_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));        \
+  } while (0)
+
+constexpr int kWgradTargetBlocks = 1024;
+constexpr int kMaxBatch = 16384;
+
+inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace
+
+struct TensorDesc {
+  std::string name;
+  int64_t offset;
+  int64_t numel;
+  int32_t shape[4];
+  int32_t ndim;
+};
+
+struct ba3c_handle {
+  ba3c_config cfg;
+  std::vector<TensorDesc> tensors;
+  int64_t flat;
+  int idx_conv[4];
+  int idx_fc1;        // first fc1 tensor
+  int idx_piW, idx_pib, idx_vW, idx_vb;
+  int per, wstride;
+  TensorTable table;
+  // timing probe
+  int probe_kernel = -1;
+  std::vector<hipEvent_t> ev_begin, ev_end;
+  int probe_used = 0;
+  int probe_launches = 0;
+  double probe_ms = 0.0;
+};
+
+namespace {
+
+// ---- workspace layout -----------------------------------------------------------------
+struct Workspace {
+  float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *sumsq;
+  uint8_t *c0, *c1, *c2;
+  unsigned long long* relu;
+  size_t bytes;
+};
+
+struct WgradPlan {
+  int M, N, K, S, kchunk, mt, nt;
+};
+
+WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN) {
+  WgradPlan w;
+  w.M = M;
+  w.N = N;
+  w.K = K;
+  w.mt = (M + BM - 1) / BM;
+  w.nt = (N + BN - 1) / BN;
+  const int ktiles = (K + GEMM_BK - 1) / GEMM_BK;
+  int S = (kWgradTargetBlocks + w.mt * w.nt - 1) / (w.mt * w.nt);
+  S = std::max(1, std::min(S, (ktiles + 3) / 4));   // >= 4 k-tiles per split
+  const int tiles_per = (ktiles + S - 1) / S;
+  w.kchunk = tiles_per * GEMM_BK;
+  w.S = (K + w.kchunk - 1) / w.kchunk;
+  return w;
+}
+
+// geometry constants (train.py:92, :177-212)
+constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
+
+size_t max_partials(const ba3c_handle* h, int B) {
+  const int C = h->cfg.channels, F = h->cfg.fc_neurons;
+  size_t mx = 0;
+  auto upd = [&](const WgradPlan& w) { mx = std::max(mx, (size_t)w.S * w.M * w.N); };
+  upd(plan_wgrad(25 * C, 32, B * 6400, 128, 32));
+  upd(plan_wgrad(800, 32, B * 1296, 128, 32));
+  upd(plan_wgrad(800, 64, B * 196, 128, 64));
+  upd(plan_wgrad(576, 64, B * 25, 128, 64));
+  upd(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
+  upd(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
+  return mx;
+}
+
+Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
+  Workspace w;
+  std::memset(&w, 0, sizeof(w));
+  char* p = static_cast<char*>(base);
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> char* {
+    char* r = p ? p + off : nullptr;
+    off += align256(bytes);
+    return r;
+  };
+  const size_t Bz = (size_t)B;
+  const int F = h->cfg.fc_neurons;
+  w.p0 = (float*)take(Bz * P0 * 4);
+  w.p1 = (float*)take(Bz * P1 * 4);
+  w.p2 = (float*)take(Bz * P2 * 4);
+  w.a3 = (float*)take(Bz * A3 * 4);
+  w.h = (float*)take(Bz * F * 4);
+  w.relu = (unsigned long long*)take(64);
+  if (train) {
+    w.c0 = (uint8_t*)take(Bz * P0);
+    w.c1 = (uint8_t*)take(Bz * P1);
+    w.c2 = (uint8_t*)take(Bz * P2);
+    w.dh = (float*)take(Bz * F * 4);
+    w.dy3 = (float*)take(Bz * A3 * 4);
+    w.dp2 = (float*)take(Bz * P2 * 4);
+    w.dp1 = (float*)take(Bz * P1 * 4);
+    w.dp0 = (float*)take(Bz * P0 * 4);
+    w.dzv = (float*)take(Bz * MAXA * 4);
+    w.terms = (float*)take(Bz * NTERMS * 4);
+    w.part = (float*)take(max_partials(h, B) * 4);
+    w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
+  } else {
+    w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
+  }
+  w.bytes = off;
+  return w;
+}
+
+// ---- launch helpers -------------------------------------------------------------------
+struct ProbeScope {
+  ba3c_handle* h;
+  hipStream_t s;
+  bool on;
+  ProbeScope(ba3c_handle* h_, hipStream_t s_, int kid) : h(h_), s(s_), on(false) {
+    if (h->probe_kernel == kid && h->probe_used < (int)h->ev_begin.size()) {
+      on = true;
+      (void)hipEventRecord(h->ev_begin[h->probe_used], s);
+    }
+  }
+  ~ProbeScope() {
+    if (on) {
+      (void)hipEventRecord(h->ev_end[h->probe_used], s);
+      h->probe_used++;
+    }
+  }
+};
+
+template <int BM, int BN, int WGM, int WGN, class P>
+int launch_gemm(ba3c_handle* h, hipStream_t s, int kid, const P& p, int splits) {
+  if (p.M <= 0 || p.N <= 0) return BA3C_OK;
+  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
+  {
+    ProbeScope ps(h, s, kid);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, P>), grid, dim3(GEMM_THREADS), 0, s, p);
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int launch_reduce(ba3c_handle* h, hipStream_t s, const float* part, int S, const ReduceMap& mp) {
+  const int MN = mp.M * mp.N;
+  {
+    ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 63) / 64), dim3(256), 0, s, part, S, mp);
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+#define CHECK(x)            \
+  do {                      \
+    int _r = (x);           \
+    if (_r != BA3C_OK) return _r; \
+  } while (0)
+
+// ---- forward --------------------------------------------------------------------------
+template <int CH>
+int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
+                const Workspace& w, bool train) {
+  const int F = h->cfg.fc_neurons;
+  const float* W0 = prm + h->tensors[h->idx_conv[0]].offset;
+  const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
+  const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
+  const float* W3 = prm + h->tensors[h->idx_conv[3]].offset;
+  unsigned long long* rc = train ? w.relu : nullptr;
+  if (train) {
+    ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> c0{state, W0, w.p0, w.c0, rc, 1.0f / 255.0f,
+                                                 B * 6400, 32, 25 * CH, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+    ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> c1{w.p0, W1, w.p1, w.c1, rc, 1.0f, B * 1296, 32, 800, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
+    ConvFwd<false, 18, 18, 32, 32, 5, 5, 64, 0> c2{w.p1, W2, w.p2, w.c2, rc, 1.0f, B * 196, 64, 800, 0};
+    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
+  } else {
+    ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
+                                                 B * 6400, 32, 25 * CH, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+    ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 1> c1{w.p0, W1, w.p1, nullptr, nullptr, 1.0f, B * 1296, 32, 800, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
+    ConvFwd<false, 18, 18, 32, 32, 5, 5, 64, 1> c2{w.p1, W2, w.p2, nullptr, nullptr, 1.0f, B * 196, 64, 800, 0};
+    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
+  }
+  ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
+  CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
+  FcFwd fc{w.a3, prm + h->tensors[h->idx_fc1].offset, w.h, rc, h->per, h->wstride,
+           h->cfg.replace_with_conv ? 0 : 1, B, F, 1600, 0};
+  CHECK((launch_gemm<128, 64, 2, 2>(h, s, BA3C_K_FC1_FWD, fc, 1)));
+  return BA3C_OK;
+}
+
+template <int CH>
+int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
+                 const Workspace& w, float* grads) {
+  const int F = h->cfg.fc_neurons, A = h->cfg.num_actions;
+  const bool legacy = !h->cfg.replace_with_conv;
+  const float* W1c = prm + h->tensors[h->idx_conv[1]].offset;
+  const float* W2c = prm + h->tensors[h->idx_conv[2]].offset;
+  const float* W3c = prm + h->tensors[h->idx_conv[3]].offset;
+  const float* Wfc = prm + h->tensors[h->idx_fc1].offset;
+
+  // heads: d fc-pi/W, fc-pi/b, fc-v/W, fc-v/b  (X = h, G = [dz | dV])
+  {
+    WgradPlan pl = plan_wgrad(F + 1, A + 1, B, 128, 32);
+    BatchWgrad g{w.h, w.dzv, w.part, F, MAXA, 1, pl.M, pl.N, pl.K, pl.kchunk};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_HEAD_WGRAD, g, pl.S)));
+    ReduceMap mp{};
+    mp.kind = 2;
+    mp.M = pl.M;
+    mp.N = pl.N;
+    mp.A = A;
+    mp.dst = grads + h->tensors[h->idx_piW].offset;
+    mp.dst_pib = grads + h->tensors[h->idx_pib].offset;
+    mp.dst_vW = grads + h->tensors[h->idx_vW].offset;
+    mp.dst_vb = grads + h->tensors[h->idx_vb].offset;
+    CHECK(launch_reduce(h, s, w.part, pl.S, mp));
+  }
+  // fc1 weight (+ legacy bias) gradient
+  {
+    WgradPlan pl = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
+    BatchWgrad g{w.a3, w.dh, w.part, 1600, F, legacy ? 1 : 0, pl.M, pl.N, pl.K, pl.kchunk};
+    CHECK((launch_gemm<128, 64, 2, 2>(h, s, BA3C_K_FC1_WGRAD, g, pl.S)));
+    ReduceMap mp{};
+    mp.kind = 1;
+    mp.M = pl.M;
+    mp.N = pl.N;
+    mp.per = h->per;
+    mp.wstride = h->wstride;
+    mp.dst = grads + h->tensors[h->idx_fc1].offset;
+    CHECK(launch_reduce(h, s, w.part, pl.S, mp));
+  }
+  // fc1 input gradient -> dY3 (ReluGrad of conv3 fused)
+  {
+    FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
+    CHECK((launch_gemm<128, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
+  }
+  auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad) {
+    ReduceMap mp{};
+    mp.kind = 0;
+    mp.M = pl.M;
+    mp.N = pl.N;
+    mp.cin = cin;
+    mp.cinpad = cinpad;
+    mp.dst = grads + h->tensors[h->idx_conv[layer]].offset;
+    return launch_reduce(h, s, w.part, pl.S, mp);
+  };
+  // conv3
+  {
+    WgradPlan pl = plan_wgrad(576, 64, B * 25, 128, 64);
+    ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_WGRAD, g, pl.S)));
+    CHECK(conv_reduce(pl, 3, 64, 64));
+    ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0};
+    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
+  }
+  // conv2
+  {
+    WgradPlan pl = plan_wgrad(800, 64, B * 196, 128, 64);
+    ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_WGRAD, g, pl.S)));
+    CHECK(conv_reduce(pl, 2, 32, 32));
+    ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
+  }
+  // conv1
+  {
+    WgradPlan pl = plan_wgrad(800, 32, B * 1296, 128, 32);
+    ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_WGRAD, g, pl.S)));
+    CHECK(conv_reduce(pl, 1, 32, 32));
+    ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
+  }
+  // conv0 (no input gradient: the frames are not trainable)
+  {
+    WgradPlan pl = plan_wgrad(25 * CH, 32, B * 6400, 128, 32);
+    ConvWgrad<true, 84, 84, CH, 5, 5, 32, true> g{state, w.dp0, w.c0, w.part, 1.0f / 255.0f, pl.M, pl.N, pl.K, pl.kchunk};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_WGRAD, g, pl.S)));
+    CHECK(conv_reduce(pl, 0, CH, 16));
+  }
+  return BA3C_OK;
+}
+
+int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, int B,
+              const int64_t* action, const float* R, float beta, float explore, bool train,
+              float* probs, float* probsT, float* value) {
+  HeadsArgs a{};
+  a.h = w.h;
+  a.piW = prm + h->tensors[h->idx_piW].offset;
+  a.pib = prm + h->tensors[h->idx_pib].offset;
+  a.vW = prm + h->tensors[h->idx_vW].offset;
+  a.vb = prm + h->tensors[h->idx_vb].offset;
+  a.action = action;
+  a.R = R;
+  a.probs = probs;
+  a.probsT = probsT;
+  a.value = value;
+  a.dzv = w.dzv;
+  a.dh = w.dh;
+  a.terms = w.terms;
+  a.B = B;
+  a.F = h->cfg.fc_neurons;
+  a.A = h->cfg.num_actions;
+  a.train = train ? 1 : 0;
+  a.legacy = h->cfg.replace_with_conv ? 0 : 1;
+  a.beta = beta;
+  a.explore = explore;
+  a.invB = 1.0f / (float)B;
+  {
+    ProbeScope ps(h, s, BA3C_K_HEADS);
+    hipLaunchKernelGGL(heads_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a);
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+bool check_ptr(const void* p) { return p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int ba3c_version(void) { return 1; }
+
+const char* ba3c_last_error(void) { return g_err.c_str(); }
+
+int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
+  if (!cfg || !out) return fail(BA3C_ERR_INVALID, "null argument");
+  const ba3c_config& c = *cfg;
+  if (c.channels != 4 && c.channels != 12)
+    return fail(BA3C_ERR_INVALID, "channels must be 4 or 12 (FRAME_HISTORY * --channels)");
+  if (c.num_actions < 1 || c.num_actions >= MAXA)
+    return fail(BA3C_ERR_INVALID, "num_actions must be in [1, 31]");
+  if (c.max_batch < 1 || c.max_batch > kMaxBatch)
+    return fail(BA3C_ERR_INVALID, "max_batch must be in [1, 16384]");
+  const int splits = c.replace_with_conv ? c.fc_splits : c.ps;
+  if (splits < 1 || c.fc_neurons < 4 || c.fc_neurons % splits != 0 || (c.fc_neurons / splits) % 4 != 0)
+    return fail(BA3C_ERR_INVALID, "fc_neurons must be a multiple of 4*fc_splits (or 4*ps)");
+  ba3c_handle* h = new ba3c_handle();
+  h->cfg = c;
+  const int F = c.fc_neurons, per = F / splits;
+  h->per = per;
+  int64_t off = 0;
+  auto add = [&](const std::string& name, std::initializer_list<int> shape) {
+    TensorDesc d;
+    d.name = name;
+    d.offset = off;
+    d.ndim = (int)shape.size();
+    int64_t n = 1;
+    int i = 0;
+    for (int v : shape) {
+      d.shape[i++] = v;
+      n *= v;
+    }
+    for (; i < 4; ++i) d.shape[i] = 0;
+    d.numel = n;
+    h->tensors.push_back(d);
+    off = align64(off + n);
+    return (int)h->tensors.size() - 1;
+  };
+  h->idx_conv[0] = add("conv0/W", {5, 5, 16, 32});
+  h->idx_conv[1] = add("conv1/W", {5, 5, 32, 32});
+  h->idx_conv[2] = add("conv2/W", {5, 5, 32, 64});
+  h->idx_conv[3] = add("conv3/W", {3, 3, 64, 64});
+  h->idx_fc1 = -1;
+  for (int i = 0; i < splits; ++i) {
+    int t;
+    if (c.replace_with_conv) {
+      t = add("fc1_" + std::to_string(i) + "/W", {5, 5, 64, per});
+    } else {
+      t = add("fc1_" + std::to_string(i) + "/W", {1600, per});
+      add("fc1_" + std::to_string(i) + "/b", {per});
+    }
+    if (i == 0) h->idx_fc1 = t;
+  }
+  h->wstride = c.replace_with_conv ? 1600 * per : (int)(1600 * per + align64(per));
+  h->idx_piW = add("fc-pi/W", {F, c.num_actions});
+  h->idx_pib = add("fc-pi/b", {c.num_actions});
+  h->idx_vW = add("fc-v/W", {F, 1});
+  h->idx_vb = add("fc-v/b", {1});
+  h->flat = off;
+  if ((int)h->tensors.size() > MAXT) {
+    delete h;
+    return fail(BA3C_ERR_INVALID, "too many tensors");
+  }
+  TensorTable& tt = h->table;
+  std::memset(&tt, 0, sizeof(tt));
+  tt.n = (int)h->tensors.size();
+  int ch = 0;
+  for (int i = 0; i < tt.n; ++i) {
+    tt.off[i] = h->tensors[i].offset;
+    tt.numel[i] = (int)h->tensors[i].numel;
+    tt.chunk0[i] = ch;
+    ch += (int)((h->tensors[i].numel + UPD_CHUNK - 1) / UPD_CHUNK);
+  }
+  tt.chunk0[tt.n] = ch;
+  tt.nchunks = ch;
+  *out = h;
+  return BA3C_OK;
+}
+
+void ba3c_destroy(ba3c_handle* h) {
+  if (!h) return;
+  for (auto e : h->ev_begin) (void)hipEventDestroy(e);
+  for (auto e : h->ev_end) (void)hipEventDestroy(e);
+  delete h;
+}
+
+int ba3c_num_tensors(const ba3c_handle* h) { return h ? (int)h->tensors.size() : 0; }
+
+int ba3c_tensor_info(const ba3c_handle* h, int32_t i, const char** name, int64_t* offset,
+                     int64_t* numel, int32_t shape[4], int32_t* ndim) {
+  if (!h || i < 0 || i >= (int)h->tensors.size()) return fail(BA3C_ERR_INVALID, "bad tensor index");
+  const TensorDesc& d = h->tensors[i];
+  if (name) *name = d.name.c_str();
+  if (offset) *offset = d.offset;
+  if (numel) *numel = d.numel;
+  if (shape)
+    for (int k = 0; k < 4; ++k) shape[k] = d.shape[k];
+  if (ndim) *ndim = d.ndim;
+  return BA3C_OK;
+}
+
+int64_t ba3c_flat_size(const ba3c_handle* h) { return h ? h->flat : 0; }
+
+size_t ba3c_workspace_size(const ba3c_handle* h, int32_t batch, int32_t train) {
+  if (!h || batch < 1) return 0;
+  return carve(h, nullptr, batch, train != 0).bytes;
+}
+
+int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                 int32_t batch, float explore_factor, void* workspace, float* probs,
+                 float* probsT, float* value) {
+  if (!h || !check_ptr(params) || !check_ptr(state) || !check_ptr(workspace))
+    return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
+  if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Workspace w = carve(h, workspace, batch, false);
+  int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, false)
+                               : run_forward<12>(h, s, params, state, batch, w, false);
+  if (r != BA3C_OK) return r;
+  return run_heads(h, s, params, w, batch, nullptr, nullptr, 0.f, explore_factor, false, probs,
+                   probsT, value);
+}
+
+int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                     const int64_t* action, const float* futurereward, int32_t batch,
+                     float entropy_beta, void* workspace, float* grads, double* scalars) {
+  if (!h || !check_ptr(params) || !check_ptr(state) || !check_ptr(workspace) || !check_ptr(grads) ||
+      !action || !futurereward)
+    return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
+  if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Workspace w = carve(h, workspace, batch, true);
+  HIP_TRY(hipMemsetAsync(grads, 0, (size_t)h->flat * 4, s));
+  HIP_TRY(hipMemsetAsync(w.relu, 0, 8, s));
+  int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, true)
+                               : run_forward<12>(h, s, params, state, batch, w, true);
+  if (r != BA3C_OK) return r;
+  CHECK(run_heads(h, s, params, w, batch, action, futurereward, entropy_beta, 1.0f, true, nullptr,
+                  nullptr, nullptr));
+  if (scalars) {
+    hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, w.terms, batch, entropy_beta,
+                       w.relu, scalars);
+    HIP_TRY(hipGetLastError());
+  }
+  return h->cfg.channels == 4 ? run_backward<4>(h, s, params, state, batch, w, grads)
+                              : run_backward<12>(h, s, params, state, batch, w, grads);
+}
+
+int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace) {
+  if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(workspace);  // first nchunks floats of any workspace
+  {
+    ProbeScope ps(h, s, BA3C_K_CLIP);
+    hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part);
+    hipLaunchKernelGGL(clip_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table,
+                       (const float*)part);
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
+                      const float* grads, float* slot0, float* slot1, const ba3c_opt_params* hp,
+                      float grad_scale, int32_t fuse_clip, void* workspace) {
+  if (!h || !hp || !check_ptr(params) || !check_ptr(grads)) return fail(BA3C_ERR_INVALID, "null pointer");
+  const bool need0 = opt != BA3C_OPT_GD, need1 = opt == BA3C_OPT_ADAM || opt == BA3C_OPT_RMS || opt == BA3C_OPT_ADADELTA;
+  if ((need0 && !check_ptr(slot0)) || (need1 && !check_ptr(slot1)))
+    return fail(BA3C_ERR_INVALID, "missing optimizer slot");
+  if (fuse_clip && !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "fuse_clip needs a workspace");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  UpdateArgs a{};
+  a.p = params;
+  a.g = grads;
+  a.s0 = slot0;
+  a.s1 = slot1;
+  a.grad_scale = grad_scale;
+  a.lr = hp->lr;
+  // TF-1.2 float32 scalar arithmetic of ApplyAdam: alpha = lr*sqrt(1-b2^t)/(1-b1^t)
+  a.alpha = (hp->lr * sqrtf(1.0f - hp->beta2_power)) / (1.0f - hp->beta1_power);
+  a.one_minus_b1 = 1.0f - hp->beta1;
+  a.one_minus_b2 = 1.0f - hp->beta2;
+  a.eps = hp->epsilon;
+  a.decay_c = 1.0f - hp->decay;
+  a.momentum = hp->momentum;
+  a.rho = hp->rho;
+  a.one_minus_rho = 1.0f - hp->rho;
+  float* part = static_cast<float*>(workspace);
+  if (fuse_clip) {
+    hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part);
+    HIP_TRY(hipGetLastError());
+    a.clip_part = part;
+  }
+  dim3 grid(h->table.nchunks);
+  {
+    ProbeScope ps(h, s, BA3C_K_UPDATE);
+    switch (opt) {
+      case BA3C_OPT_ADAM: hipLaunchKernelGGL(update_kernel<0>, grid, dim3(256), 0, s, a, h->table); break;
+      case BA3C_OPT_GD: hipLaunchKernelGGL(update_kernel<1>, grid, dim3(256), 0, s, a, h->table); break;
+      case BA3C_OPT_ADAGRAD: hipLaunchKernelGGL(update_kernel<2>, grid, dim3(256), 0, s, a, h->table); break;
+      case BA3C_OPT_ADADELTA: hipLaunchKernelGGL(update_kernel<3>, grid, dim3(256), 0, s, a, h->table); break;
+      case BA3C_OPT_MOMENTUM: hipLaunchKernelGGL(update_kernel<4>, grid, dim3(256), 0, s, a, h->table); break;
+      case BA3C_OPT_RMS: hipLaunchKernelGGL(update_kernel<5>, grid, dim3(256), 0, s, a, h->table); break;
+      default: return fail(BA3C_ERR_INVALID, "unknown optimizer id");
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_sample(void* stream, const float* probs, const double* u, int32_t batch,
+                int32_t num_actions, int64_t* actions, int32_t* nonfinite) {
+  if (!probs || !u || !actions) return fail(BA3C_ERR_INVALID, "null pointer");
+  if (batch < 0 || num_actions < 1 || num_actions >= MAXA) return fail(BA3C_ERR_INVALID, "bad shape");
+  if (batch == 0) return BA3C_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(sample_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, probs, u, batch,
+                     num_actions, actions, nonfinite);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id) {
+  if (!h) return fail(BA3C_ERR_INVALID, "null handle");
+  if (kernel_id >= BA3C_NUM_KERNELS) return fail(BA3C_ERR_INVALID, "bad kernel id");
+  if (h->ev_begin.empty() && kernel_id >= 0) {
+    h->ev_begin.resize(4096);
+    h->ev_end.resize(4096);
+    for (size_t i = 0; i < h->ev_begin.size(); ++i) {
+      HIP_TRY(hipEventCreate(&h->ev_begin[i]));
+      HIP_TRY(hipEventCreate(&h->ev_end[i]));
+    }
+  }
+  h->probe_kernel = kernel_id;
+  h->probe_used = 0;
+  h->probe_ms = 0.0;
+  h->probe_launches = 0;
+  return BA3C_OK;
+}
+
+int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches) {
+  if (!h) return fail(BA3C_ERR_INVALID, "null handle");
+  for (int i = 0; i < h->probe_used; ++i) {
+    HIP_TRY(hipEventSynchronize(h->ev_end[i]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev_begin[i], h->ev_end[i]));
+    h->probe_ms += ms;
+    h->probe_launches++;
+  }
+  h->probe_used = 0;
+  if (total_ms) *total_ms = h->probe_ms;
+  if (launches) *launches = h->probe_launches;
+  return BA3C_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+// ba3c_gemm.h — fp32-MFMA implicit-GEMM engine for gfx950 (CDNA4).
+//
+// Every conv / FC product of the BA3C net (OpenAIGym/train.py:177-264 forward, and the TF
+// autodiff Conv2DBackpropInput / Conv2DBackpropFilter / MatMul grads of
+// train/multigpu.py:85-86) is C[M][N] = sum_k A[m][k] B[k][n] where A and B are gathered
+// on the fly from NHWC activations / HWIO weights by a problem struct P (ba3c_problems.h).
+//
+// Tile: BM x BN x 32 per 256-thread workgroup (4 waves as WGM x WGN), each wave owning a
+// (BM/WGM) x (BN/WGN) block of 32x32 accumulators fed by v_mfma_f32_32x32x2_f32 (exact f32,
+// 64 FLOP/clk/SIMD — gfx950 has no xf32).  Operands are staged through LDS in k-major
+// layout ([k][m], [k][n]) so every MFMA fragment read is one conflict-free ds_read_b32 per
+// 32-lane half; gathered rows that are contiguous along k are transposed on the LDS write
+// (row pitch BM+1 keeps those ds_write_b32 conflict-free).  The next k-tile's global loads
+// are issued before the current tile's MFMAs (register prefetch, one LDS buffer).
+// Split-K over blockIdx.z (P::kchunk > 0) writes fp32 partial slabs reduced by a separate,
+// deterministic kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ba3c {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int GEMM_BK = 32;
+constexpr int GEMM_THREADS = 256;
+
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+__device__ __forceinline__ float f4get(const float4& v, int j) {
+  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+template <int BM, int BN, int WGM, int WGN, class P>
+__global__ void __launch_bounds__(GEMM_THREADS) gemm_kernel(const P p) {
+  static_assert(WGM * WGN == 4, "4 waves per workgroup");
+  constexpr int BK = GEMM_BK;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "wave tile");
+  constexpr int PADA = P::A_KCONTIG ? 1 : 4;
+  constexpr int PADB = P::B_KCONTIG ? 1 : 4;
+  constexpr int LDA = BM + PADA, LDB = BN + PADB;
+  constexpr int NA = BM * BK / 4 / GEMM_THREADS;  // float4 per thread per k-tile
+  constexpr int NB = BN * BK / 4 / GEMM_THREADS;
+  static_assert(NA >= 1 && NB >= 1, "tile too small for 256 threads");
+  // !KCONTIG operands: a float4 spans 4 consecutive m (n); QA quads per k-row.
+  constexpr int QA = BM / 4, QB = BN / 4;
+  constexpr int RA = GEMM_THREADS / QA, RB = GEMM_THREADS / QB;  // k-rows per pass
+
+  __shared__ __attribute__((aligned(16))) float lds[BK * LDA + BK * LDB];
+  float* As = lds;
+  float* Bs = lds + BK * LDA;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  int kbeg = 0, kend = p.K;
+  if (p.kchunk > 0) {
+    kbeg = blockIdx.z * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
+
+  // per-thread operand coordinates that do not change along k
+  typename P::ARow arow[P::A_KCONTIG ? NA : 1];
+  typename P::BRow brow[P::B_KCONTIG ? NB : 1];
+  if constexpr (P::A_KCONTIG) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) arow[i] = p.a_row(m0 + (tid >> 3) + 32 * i);
+  } else {
+    arow[0] = p.a_col(m0 + (tid % QA) * 4);
+  }
+  if constexpr (P::B_KCONTIG) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) brow[i] = p.b_row(n0 + (tid >> 3) + 32 * i);
+  } else {
+    brow[0] = p.b_col(n0 + (tid % QB) * 4);
+  }
+
+  float4 ra[NA], rb[NB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      if constexpr (P::A_KCONTIG)
+        ra[i] = p.a_load(arow[i], k0 + (tid & 7) * 4, kend);
+      else
+        ra[i] = p.a_load_t(arow[0], k0 + tid / QA + RA * i, kend);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (P::B_KCONTIG)
+        rb[i] = p.b_load(brow[i], k0 + (tid & 7) * 4, kend);
+      else
+        rb[i] = p.b_load_t(brow[0], k0 + tid / QB + RB * i, kend);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      if constexpr (P::A_KCONTIG) {
+        const int ml = (tid >> 3) + 32 * i, kq = (tid & 7) * 4;
+        As[(kq + 0) * LDA + ml] = ra[i].x;
+        As[(kq + 1) * LDA + ml] = ra[i].y;
+        As[(kq + 2) * LDA + ml] = ra[i].z;
+        As[(kq + 3) * LDA + ml] = ra[i].w;
+      } else {
+        const int kl = tid / QA + RA * i, mq = (tid % QA) * 4;
+        *reinterpret_cast<float4*>(&As[kl * LDA + mq]) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (P::B_KCONTIG) {
+        const int nl = (tid >> 3) + 32 * i, kq = (tid & 7) * 4;
+        Bs[(kq + 0) * LDB + nl] = rb[i].x;
+        Bs[(kq + 1) * LDB + nl] = rb[i].y;
+        Bs[(kq + 2) * LDB + nl] = rb[i].z;
+        Bs[(kq + 3) * LDB + nl] = rb[i].w;
+      } else {
+        const int kl = tid / QB + RB * i, nq = (tid % QB) * 4;
+        *reinterpret_cast<float4*>(&Bs[kl * LDB + nq]) = rb[i];
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int li = lane & 31, lh = lane >> 5;
+  const float* Aw = As + wm * WTM + li;
+  const float* Bw = Bs + wn * WTN + li;
+
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    store();
+    __syncthreads();
+    if (k0 + BK < kend) load(k0 + BK);
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      const int kr = 2 * s + lh;
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) av[a] = Aw[kr * LDA + a * 32];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bv[b] = Bw[kr * LDB + b * 32];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  p.template epilogue<TM, TN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, blockIdx.z);
+}
+
+// C/D layout of a 32x32 block (v_mfma_f32_32x32x2_f32): lane l holds column (l & 31),
+// register r holds row (r & 3) + 8 * (r >> 2) + 4 * (l >> 5).
+__device__ __forceinline__ int acc_row(int r, int lane) {
+  return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace ba3c

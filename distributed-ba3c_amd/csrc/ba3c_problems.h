@@ -1,0 +1,417 @@
+// ba3c_problems.h — operand gathers and fused epilogues for each product of the BA3C net.
+//
+// Geometry is compile-time (84x84 frames, train.py:92; conv stack train.py:177-212), so all
+// index decodes are multiply-shift.  Activations are NHWC fp32; a max-pooled layer stores
+// its pooled output plus a 1-byte argmax code per element (0..3 = row-major position of
+// the FIRST maximum of the 2x2 window, TF's tie rule; 255 = window max <= 0, i.e. the ReLU
+// gradient is zero).  Backward loaders "unpool" on the fly from (dP, code), so no
+// full-resolution gradient map is ever written.
+#pragma once
+#include "ba3c_gemm.h"
+
+namespace ba3c {
+
+__device__ __forceinline__ float4 u8x4_to_f4(uint32_t v) {
+  return make_float4((float)(v & 255u), (float)((v >> 8) & 255u), (float)((v >> 16) & 255u),
+                     (float)(v >> 24));
+}
+
+// dY at conv-output position (y, x) from pooled grad dP and argmax codes.
+template <int PW, int COUT>
+__device__ __forceinline__ float4 unpool4(const float* __restrict__ dP, const uint8_t* __restrict__ code,
+                                          int n_ph_base, int y, int x, int c) {
+  const int pidx = n_ph_base + (y >> 1) * PW + (x >> 1);
+  const uint32_t sub = ((y & 1) << 1) | (x & 1);
+  float4 g = *reinterpret_cast<const float4*>(dP + (size_t)pidx * COUT + c);
+  const uint32_t cd = *reinterpret_cast<const uint32_t*>(code + (size_t)pidx * COUT + c);
+  g.x = ((cd & 255u) == sub) ? g.x : 0.f;
+  g.y = (((cd >> 8) & 255u) == sub) ? g.y : 0.f;
+  g.z = (((cd >> 16) & 255u) == sub) ? g.z : 0.f;
+  g.w = ((cd >> 24) == sub) ? g.w : 0.f;
+  return g;
+}
+
+// ------------------------------------------------------------------------------------
+// Forward conv (Conv2D VALID stride 1, no bias; models/conv2d.py:63-73, train.py:177-212)
+// MODE 0: ReLU + 2x2 max-pool + argmax code (training)   MODE 1: same without codes
+// MODE 2: ReLU only, plain NHWC store (conv3)
+// M rows: MODE 0/1 = (n, ph, pw, sub) so a lane's 4 consecutive accumulator rows are one
+// pooling window; MODE 2 = (n, oh, ow).  K = (kh, kw, c) over the REAL input channels
+// (conv0's 16-channel zero padding, train.py:173-174, contributes exactly 0).
+// ------------------------------------------------------------------------------------
+template <bool SRC_U8, int HIN, int WIN, int CIN, int CINPAD, int KH, int KW, int COUT, int MODE>
+struct ConvFwd {
+  static constexpr bool A_KCONTIG = true, B_KCONTIG = false;
+  static constexpr int HO = HIN - KH + 1, WO = WIN - KW + 1, PH = HO / 2, PW = WO / 2;
+  static constexpr int KDIM = KH * KW * CIN;
+  using ARow = int;
+  using BRow = int;
+  const void* src;
+  const float* w;
+  float* out;
+  uint8_t* code;
+  unsigned long long* relu_count;
+  float scale;
+  int M, N, K, kchunk;
+
+  __device__ int a_row(int m) const {
+    if (m >= M) return -1;
+    int n, oh, ow;
+    if constexpr (MODE != 2) {
+      const int win = m >> 2, sub = m & 3;
+      n = win / (PH * PW);
+      const int r = win - n * (PH * PW);
+      const int ph = r / PW, pw = r - ph * PW;
+      oh = 2 * ph + (sub >> 1);
+      ow = 2 * pw + (sub & 1);
+    } else {
+      n = m / (HO * WO);
+      const int r = m - n * (HO * WO);
+      oh = r / WO;
+      ow = r - oh * WO;
+    }
+    return ((n * HIN + oh) * WIN + ow) * CIN;
+  }
+  __device__ float4 a_load(int row, int k, int kend) const {
+    if (row < 0 || k >= kend) return f4zero();
+    const int kh = k / (KW * CIN);
+    const int r = k - kh * (KW * CIN);
+    const int kw = r / CIN, c = r - kw * CIN;
+    const int off = row + (kh * WIN + kw) * CIN + c;
+    if constexpr (SRC_U8)
+      return u8x4_to_f4(*reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(src) + off));
+    else
+      return *reinterpret_cast<const float4*>(static_cast<const float*>(src) + off);
+  }
+  __device__ int b_col(int n) const { return n < N ? n : -1; }
+  __device__ float4 b_load_t(int ncol, int k, int kend) const {
+    if (ncol < 0 || k >= kend) return f4zero();
+    const int kh = k / (KW * CIN);
+    const int r = k - kh * (KW * CIN);
+    const int kw = r / CIN, c = r - kw * CIN;
+    return *reinterpret_cast<const float4*>(w + ((kh * KW + kw) * CINPAD + c) * COUT + ncol);
+  }
+  template <int TM, int TN>
+  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
+    const int j = lane & 31, h = lane >> 5;
+    unsigned long long pos = 0;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = ncol + b * 32 + j;
+        if constexpr (MODE != 2) {
+          const int wbase = (mrow + a * 32) >> 2;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v0 = acc[a][b][4 * q + 0] * scale, v1 = acc[a][b][4 * q + 1] * scale;
+            const float v2 = acc[a][b][4 * q + 2] * scale, v3 = acc[a][b][4 * q + 3] * scale;
+            pos += (v0 > 0.f) + (v1 > 0.f) + (v2 > 0.f) + (v3 > 0.f);
+            float mx = v0;
+            uint32_t arg = 0;
+            if (v1 > mx) { mx = v1; arg = 1; }
+            if (v2 > mx) { mx = v2; arg = 2; }
+            if (v3 > mx) { mx = v3; arg = 3; }
+            const int win = wbase + 2 * q + h;
+            if (win * 4 < M && col < N) {
+              out[(size_t)win * COUT + col] = fmaxf(mx, 0.f);
+              if constexpr (MODE == 0) code[(size_t)win * COUT + col] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow + a * 32 + acc_row(r, lane);
+            const float v = acc[a][b][r] * scale;
+            pos += (v > 0.f);
+            if (m < M && col < N) out[(size_t)m * COUT + col] = fmaxf(v, 0.f);
+          }
+        }
+      }
+    if (relu_count) {
+      pos = wave_sum_u64(pos);
+      if (lane == 0 && pos) atomicAdd(relu_count, pos);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// Conv2DBackpropInput: dX[n,y,x,ci] = sum_{kh,kw,o} dY[n,y-kh,x-kw,o] W[kh,kw,ci,o]
+// M = (n, y, x) over the input map, N = ci, K = (kh, kw, o).  POOLED: dY is unpooled from
+// (dP, code) of the max-pool that follows this conv (MaxPoolGrad + ReluGrad fused).
+// ------------------------------------------------------------------------------------
+template <int HIN, int WIN, int CIN, int KH, int KW, int COUT, bool POOLED>
+struct ConvDgrad {
+  static constexpr bool A_KCONTIG = true, B_KCONTIG = true;
+  static constexpr int HO = HIN - KH + 1, WO = WIN - KW + 1, PH = HO / 2, PW = WO / 2;
+  struct ARow { int n, y, x; };
+  using BRow = int;
+  const float* dy;       // POOLED: dP [B,PH,PW,COUT]  else dY [B,HO,WO,COUT]
+  const uint8_t* code;   // POOLED only
+  const float* w;        // [KH,KW,CIN,COUT]
+  float* dx;             // [B,HIN,WIN,CIN]
+  int M, N, K, kchunk;
+
+  __device__ ARow a_row(int m) const {
+    ARow r;
+    if (m >= M) { r.n = -1; r.y = 0; r.x = 0; return r; }
+    r.n = m / (HIN * WIN);
+    const int q = m - r.n * (HIN * WIN);
+    r.y = q / WIN;
+    r.x = q - r.y * WIN;
+    return r;
+  }
+  __device__ float4 a_load(const ARow& r, int k, int kend) const {
+    if (r.n < 0 || k >= kend) return f4zero();
+    const int kh = k / (KW * COUT);
+    const int q = k - kh * (KW * COUT);
+    const int kw = q / COUT, o = q - kw * COUT;
+    const int yy = r.y - kh, xx = r.x - kw;
+    if (yy < 0 || yy >= HO || xx < 0 || xx >= WO) return f4zero();
+    if constexpr (POOLED)
+      return unpool4<PW, COUT>(dy, code, r.n * (PH * PW), yy, xx, o);
+    else
+      return *reinterpret_cast<const float4*>(dy + ((size_t)(r.n * HO + yy) * WO + xx) * COUT + o);
+  }
+  __device__ int b_row(int n) const { return n < N ? n : -1; }
+  __device__ float4 b_load(int ci, int k, int kend) const {
+    if (ci < 0 || k >= kend) return f4zero();
+    const int kh = k / (KW * COUT);
+    const int q = k - kh * (KW * COUT);
+    const int kw = q / COUT, o = q - kw * COUT;
+    return *reinterpret_cast<const float4*>(w + ((kh * KW + kw) * CIN + ci) * COUT + o);
+  }
+  template <int TM, int TN>
+  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
+    const int j = lane & 31;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = ncol + b * 32 + j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow + a * 32 + acc_row(r, lane);
+          if (m < M && col < N) dx[(size_t)m * CIN + col] = acc[a][b][r];
+        }
+      }
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// Conv2DBackpropFilter: dW[kh,kw,c,o] = sum_{n,y,x} X[n,y+kh,x+kw,c] dY[n,y,x,o]
+// M = (kh, kw, c) (real channels), N = o, K = (n, y, x) split over blockIdx.z.
+// Writes fp32 partial slabs part[z][m][n]; scale = 1/255 for the uint8 frame input.
+// ------------------------------------------------------------------------------------
+template <bool SRC_U8, int HIN, int WIN, int CIN, int KH, int KW, int COUT, bool POOLED>
+struct ConvWgrad {
+  static constexpr bool A_KCONTIG = false, B_KCONTIG = false;
+  static constexpr int HO = HIN - KH + 1, WO = WIN - KW + 1, PH = HO / 2, PW = WO / 2;
+  using ARow = int;
+  using BRow = int;
+  const void* src;       // X [B,HIN,WIN,CIN] (u8 or f32)
+  const float* dy;       // POOLED: dP [B,PH,PW,COUT] else dY [B,HO,WO,COUT]
+  const uint8_t* code;
+  float* part;
+  float scale;
+  int M, N, K, kchunk;
+
+  __device__ int a_col(int m) const {
+    if (m >= M) return -1;
+    const int kh = m / (KW * CIN);
+    const int q = m - kh * (KW * CIN);
+    const int kw = q / CIN, c = q - kw * CIN;
+    return (kh * WIN + kw) * CIN + c;
+  }
+  __device__ float4 a_load_t(int mo, int k, int kend) const {
+    if (mo < 0 || k >= kend) return f4zero();
+    const int n = k / (HO * WO);
+    const int q = k - n * (HO * WO);
+    const int y = q / WO, x = q - y * WO;
+    const size_t off = ((size_t)(n * HIN + y) * WIN + x) * CIN + mo;
+    if constexpr (SRC_U8)
+      return u8x4_to_f4(*reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(src) + off));
+    else
+      return *reinterpret_cast<const float4*>(static_cast<const float*>(src) + off);
+  }
+  __device__ int b_col(int n) const { return n < N ? n : -1; }
+  __device__ float4 b_load_t(int c, int k, int kend) const {
+    if (c < 0 || k >= kend) return f4zero();
+    const int n = k / (HO * WO);
+    const int q = k - n * (HO * WO);
+    const int y = q / WO, x = q - y * WO;
+    if constexpr (POOLED)
+      return unpool4<PW, COUT>(dy, code, n * (PH * PW), y, x, c);
+    else
+      return *reinterpret_cast<const float4*>(dy + (size_t)k * COUT + c);
+  }
+  template <int TM, int TN>
+  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int z) const {
+    const int j = lane & 31;
+    float* pz = part + (size_t)z * M * N;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = ncol + b * 32 + j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow + a * 32 + acc_row(r, lane);
+          if (m < M && col < N) pz[(size_t)m * N + col] = acc[a][b][r] * scale;
+        }
+      }
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// FC1 forward (train.py:216-243): h[b][f] = sum_j a3[b][j] W1[j][f], W1 = concat of the
+// S split tensors along f (each [1600, per], row-major; the 5x5x64 conv form flattens
+// (h,w,c) exactly like batch_flatten).  Legacy (--use_normal_fc): + bias, ReLU.
+// ------------------------------------------------------------------------------------
+struct FcFwd {
+  static constexpr bool A_KCONTIG = true, B_KCONTIG = false;
+  using ARow = int;
+  using BRow = int;
+  const float* a3;      // [B,1600]
+  const float* w1;      // split 0 base
+  float* h;             // [B,F]
+  unsigned long long* relu_count;
+  int per, wstride, legacy;
+  int M, N, K, kchunk;
+
+  __device__ int a_row(int m) const { return m < M ? m * 1600 : -1; }
+  __device__ float4 a_load(int row, int k, int kend) const {
+    if (row < 0 || k >= kend) return f4zero();
+    return *reinterpret_cast<const float4*>(a3 + (size_t)row + k);
+  }
+  __device__ int b_col(int n) const {
+    if (n >= N) return -1;
+    const int s = n / per;
+    return s * wstride + (n - s * per);
+  }
+  __device__ float4 b_load_t(int c, int k, int kend) const {
+    if (c < 0 || k >= kend) return f4zero();
+    return *reinterpret_cast<const float4*>(w1 + c + (size_t)k * per);
+  }
+  template <int TM, int TN>
+  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
+    const int j = lane & 31;
+    unsigned long long pos = 0;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = ncol + b * 32 + j;
+        float bias = 0.f;
+        if (legacy && col < N) {
+          const int s = col / per;
+          bias = w1[s * wstride + 1600 * per + (col - s * per)];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow + a * 32 + acc_row(r, lane);
+          float v = acc[a][b][r];
+          if (legacy) {
+            v = fmaxf(v + bias, 0.f);
+            pos += (v > 0.f) && (m < M);
+          }
+          if (m < M && col < N) h[(size_t)m * N + col] = v;
+        }
+      }
+    if (legacy && relu_count) {
+      pos = wave_sum_u64(pos);
+      if (lane == 0 && pos) atomicAdd(relu_count, pos);
+    }
+  }
+};
+
+// FC1 input gradient: dY3[b][j] = (sum_f dh[b][f] W1[j][f]) * (a3[b][j] > 0)
+struct FcDgrad {
+  static constexpr bool A_KCONTIG = true, B_KCONTIG = true;
+  using ARow = int;
+  using BRow = int;
+  const float* dh;   // [B,F]
+  const float* w1;
+  const float* a3;   // [B,1600] relu mask source
+  float* dy3;        // [B,1600]
+  int per, wstride;
+  int M, N, K, kchunk;  // M=B, N=1600, K=F
+
+  __device__ int a_row(int m) const { return m < M ? m * K : -1; }
+  __device__ float4 a_load(int row, int k, int kend) const {
+    if (row < 0 || k >= kend) return f4zero();
+    return *reinterpret_cast<const float4*>(dh + (size_t)row + k);
+  }
+  __device__ int b_row(int n) const { return n < N ? n * per : -1; }
+  __device__ float4 b_load(int row, int k, int kend) const {
+    if (row < 0 || k >= kend) return f4zero();
+    const int s = k / per;
+    return *reinterpret_cast<const float4*>(w1 + (size_t)s * wstride + row + (k - s * per));
+  }
+  template <int TM, int TN>
+  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
+    const int j = lane & 31;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = ncol + b * 32 + j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow + a * 32 + acc_row(r, lane);
+          if (m < M && col < N) {
+            const size_t o = (size_t)m * 1600 + col;
+            dy3[o] = a3[o] > 0.f ? acc[a][b][r] : 0.f;
+          }
+        }
+      }
+  }
+};
+
+// Weight gradient of a [B,Kin] x [Kin,Nout] product with the batch as reduction:
+// part[z][m][n] = sum_b X[b][m] G[b][n] over the chunk; row m == Kin is the bias row
+// (X == 1) when has_bias.  Used for fc1 (X=a3, G=dh) and the heads (X=h, G=[dz|dv]).
+struct BatchWgrad {
+  static constexpr bool A_KCONTIG = false, B_KCONTIG = false;
+  using ARow = int;
+  using BRow = int;
+  const float* x;    // [B, kin]
+  const float* g;    // [B, gld]
+  float* part;
+  int kin, gld, has_bias;
+  int M, N, K, kchunk;   // M = kin (+1), N = columns of g used, K = B
+
+  __device__ int a_col(int m) const {
+    if (m < kin) return m;
+    if (has_bias && m == kin) return -2;
+    return -1;
+  }
+  __device__ float4 a_load_t(int c, int k, int kend) const {
+    if (c == -1 || k >= kend) return f4zero();
+    if (c == -2) return make_float4(1.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(x + (size_t)k * kin + c);
+  }
+  __device__ int b_col(int n) const { return n < N ? n : -1; }
+  __device__ float4 b_load_t(int c, int k, int kend) const {
+    if (c < 0 || k >= kend) return f4zero();
+    return *reinterpret_cast<const float4*>(g + (size_t)k * gld + c);
+  }
+  template <int TM, int TN>
+  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int z) const {
+    const int j = lane & 31;
+    float* pz = part + (size_t)z * M * N;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = ncol + b * 32 + j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mrow + a * 32 + acc_row(r, lane);
+          if (m < M && col < N) pz[(size_t)m * N + col] = acc[a][b][r];
+        }
+      }
+  }
+};
+
+}  // namespace ba3c

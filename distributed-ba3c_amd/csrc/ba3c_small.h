@@ -1,0 +1,420 @@
+// ba3c_small.h — HBM/latency-bound kernels of the BA3C step: policy/value heads + softmax +
+// A3C loss + its gradient (train.py:250-327), scalar reduction, deterministic split-K
+// reduction of weight gradients, tf.clip_by_average_norm (train.py:329-330), the TF-1.2
+// optimizer applies (train.py:582-597) and numpy-exact action sampling (train.py:382).
+#pragma once
+#include "ba3c_gemm.h"
+
+namespace ba3c {
+
+constexpr int MAXA = 32;        // dz|dv row pitch; num_actions <= 31
+constexpr int NTERMS = 8;       // per-sample loss terms
+constexpr int MAXT = 48;        // max tensors in the flat layout
+constexpr int UPD_CHUNK = 4096; // floats per workgroup in clip / update kernels
+
+// ---------------------------------------------------------------------------------------
+// Heads: one wave per sample.  z = h W_pi + b_pi, V = h W_v + b_v, p = softmax(z),
+// pT = softmax(z * explore_factor); in training also the loss terms and
+//   dL/dp_k = [adv [k==a]/(p_k+1e-6) + beta (log(p_k+1e-6) + p_k/(p_k+1e-6))] / B
+//   dz_k = p_k (dL/dp_k - sum_j p_j dL/dp_j),  dV = (V - R) / B,
+//   dh_f = sum_k dz_k W_pi[f][k] + dV W_v[f]  (x (h_f > 0) for the legacy ReLU FC).
+// terms[n] = {log(p_a+1e-6)*adv, sum p log(p+1e-6), (V-R)^2, adv, V, max p, 0, 0}
+// ---------------------------------------------------------------------------------------
+struct HeadsArgs {
+  const float* h;
+  const float* piW;
+  const float* pib;
+  const float* vW;
+  const float* vb;
+  const int64_t* action;
+  const float* R;
+  float* probs;
+  float* probsT;
+  float* value;
+  float* dzv;
+  float* dh;
+  float* terms;
+  int B, F, A, train, legacy;
+  float beta, explore, invB;
+};
+
+__global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= p.B) return;
+  const int A = p.A;
+  float acc[MAXA];
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) acc[a] = 0.f;
+  float accv = 0.f;
+  const float* hn = p.h + (size_t)n * p.F;
+  for (int f = lane; f < p.F; f += 64) {
+    const float hv = hn[f];
+    const float* wr = p.piW + (size_t)f * A;
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a)
+      if (a < A) acc[a] = fmaf(hv, wr[a], acc[a]);
+    accv = fmaf(hv, p.vW[f], accv);
+  }
+  float z[MAXA];
+  float zmax = -INFINITY;
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) {
+    if (a < A) {
+      z[a] = wave_sum_f(acc[a]) + p.pib[a];
+      zmax = fmaxf(zmax, z[a]);
+    } else {
+      z[a] = 0.f;
+    }
+  }
+  const float V = wave_sum_f(accv) + p.vb[0];
+  // softmax(z)  (tf.nn.softmax: exp(z - max) / sum)
+  float pr[MAXA];
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) {
+    pr[a] = a < A ? expf(z[a] - zmax) : 0.f;
+    s += pr[a];
+  }
+  float pmax = 0.f;
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) {
+    pr[a] = a < A ? pr[a] / s : 0.f;
+    pmax = fmaxf(pmax, pr[a]);
+  }
+  if (p.probsT) {
+    float zt[MAXA];
+    float ztmax = -INFINITY, st = 0.f;
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a) {
+      zt[a] = z[a] * p.explore;
+      if (a < A) ztmax = fmaxf(ztmax, zt[a]);
+    }
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a) {
+      zt[a] = a < A ? expf(zt[a] - ztmax) : 0.f;
+      st += zt[a];
+    }
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a)
+      if (a < A && lane == a) p.probsT[(size_t)n * A + a] = zt[a] / st;
+  }
+  if (p.probs) {
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a)
+      if (a < A && lane == a) p.probs[(size_t)n * A + a] = pr[a];
+  }
+  if (p.value && lane == 0) p.value[n] = V;
+  if (!p.train) return;
+
+  const float Rn = p.R[n];
+  const int act = (int)p.action[n];
+  const float adv = V - Rn;
+  float gp[MAXA];
+  float lpa = 0.f, xent = 0.f, sgp = 0.f;
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) {
+    if (a < A) {
+      const float pe = pr[a] + 1e-6f;
+      const float lp = logf(pe);
+      xent += pr[a] * lp;
+      if (a == act) lpa = lp;
+      gp[a] = ((a == act ? adv / pe : 0.f) + p.beta * (lp + pr[a] / pe)) * p.invB;
+      sgp += gp[a] * pr[a];
+    } else {
+      gp[a] = 0.f;
+    }
+  }
+  float dz[MAXA];
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) dz[a] = a < A ? pr[a] * (gp[a] - sgp) : 0.f;
+  const float dV = (V - Rn) * p.invB;
+  // [dz | dV | 0...] row for the head weight-gradient product
+  {
+    float mine = 0.f;
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a)
+      if (lane == a) mine = dz[a];
+    if (lane == A) mine = dV;
+    if (lane < MAXA) p.dzv[(size_t)n * MAXA + lane] = mine;
+  }
+  float* dhn = p.dh + (size_t)n * p.F;
+  for (int f = lane; f < p.F; f += 64) {
+    const float* wr = p.piW + (size_t)f * A;
+    float g = dV * p.vW[f];
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a)
+      if (a < A) g = fmaf(dz[a], wr[a], g);
+    if (p.legacy && !(hn[f] > 0.f)) g = 0.f;
+    dhn[f] = g;
+  }
+  if (lane < NTERMS) {
+    float t = 0.f;
+    t = lane == 0 ? lpa * adv : t;
+    t = lane == 1 ? xent : t;
+    t = lane == 2 ? (V - Rn) * (V - Rn) : t;
+    t = lane == 3 ? adv : t;
+    t = lane == 4 ? V : t;
+    t = lane == 5 ? pmax : t;
+    p.terms[(size_t)n * NTERMS + lane] = t;
+  }
+}
+
+// Deterministic reduction of the per-sample terms into the TfDictOp scalars.
+__global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B, float beta,
+                                                      const unsigned long long* relu_count,
+                                                      double* out) {
+  __shared__ double red[6][256];
+  const int t = threadIdx.x;
+  double s[6] = {0, 0, 0, 0, 0, 0};
+  double mx = 0.0;
+  for (int n = t; n < B; n += 256) {
+    const float* tn = terms + (size_t)n * NTERMS;
+    s[0] += tn[0];
+    s[1] += tn[1];
+    s[2] += tn[2];
+    s[3] += tn[3];
+    s[4] += tn[4];
+    mx = fmax(mx, (double)tn[5]);
+  }
+  for (int i = 0; i < 5; ++i) red[i][t] = s[i];
+  red[5][t] = mx;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w) {
+      for (int i = 0; i < 5; ++i) red[i][t] += red[i][t + w];
+      red[5][t] = fmax(red[5][t], red[5][t + w]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double Bd = (double)B, b = (double)beta;
+    const double pl = red[0][0], xe = red[1][0], vl = red[2][0] * 0.5;
+    out[0] = (pl + xe * b + vl) / Bd;
+    out[1] = pl * 128.0 / Bd;
+    out[2] = xe * 128.0 / Bd * b;
+    out[3] = vl * 128.0 / Bd;
+    out[4] = red[3][0] / Bd;
+    out[5] = red[4][0] / Bd;
+    out[6] = red[5][0];
+    out[7] = relu_count ? (double)(*relu_count) : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Split-K weight-gradient reduction: out(m, n) = sum_z part[z][m][n] in a fixed order
+// (z mod 4 lanes, then ((s0+s1)+s2)+s3), scattered into the flat gradient layout.
+// ---------------------------------------------------------------------------------------
+struct ReduceMap {
+  int kind;          // 0 conv HWIO, 1 fc1 split, 2 heads
+  int M, N;
+  int cin, cinpad;   // conv: m = (kh*KW+kw)*cin + c  ->  ((kh*KW+kw)*cinpad + c)*N + n
+  int per, wstride;  // fc1: split s = n / per
+  int A;             // heads
+  float* dst;        // conv/fc1: tensor base; heads: fc-pi/W
+  float* dst_pib;
+  float* dst_vW;
+  float* dst_vb;
+};
+
+__device__ __forceinline__ void reduce_store(const ReduceMap& mp, int m, int n, float v) {
+  if (mp.kind == 0) {
+    const int kk = m / mp.cin, c = m - kk * mp.cin;
+    mp.dst[((size_t)kk * mp.cinpad + c) * mp.N + n] = v;
+  } else if (mp.kind == 1) {
+    const int s = n / mp.per, fl = n - s * mp.per;
+    mp.dst[(size_t)s * mp.wstride + (size_t)m * mp.per + fl] = v;  // m == 1600: legacy bias
+  } else {
+    const int F = mp.M - 1;
+    if (m < F) {
+      if (n < mp.A) mp.dst[(size_t)m * mp.A + n] = v;
+      else if (n == mp.A) mp.dst_vW[m] = v;
+    } else {
+      if (n < mp.A) mp.dst_pib[n] = v;
+      else if (n == mp.A) mp.dst_vb[0] = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int S,
+                                                           const ReduceMap mp) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, zg = threadIdx.x >> 6;
+  const int MN = mp.M * mp.N;
+  const int o = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (o < MN) {
+    int z = zg;
+    for (; z + 12 < S; z += 16) {
+      const float a0 = part[(size_t)z * MN + o], a1 = part[(size_t)(z + 4) * MN + o];
+      const float a2 = part[(size_t)(z + 8) * MN + o], a3 = part[(size_t)(z + 12) * MN + o];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; z < S; z += 4) s += part[(size_t)z * MN + o];
+  }
+  red[zg][lane] = s;
+  __syncthreads();
+  if (zg == 0 && o < MN) {
+    const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    reduce_store(mp, o / mp.N, o % mp.N, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Flat-buffer tensor table and the clip / optimizer kernels (one workgroup per chunk of
+// UPD_CHUNK floats of one tensor).
+// ---------------------------------------------------------------------------------------
+struct TensorTable {
+  int n;
+  int nchunks;
+  long long off[MAXT];
+  int numel[MAXT];
+  int chunk0[MAXT + 1];
+};
+
+__device__ __forceinline__ int table_find(const TensorTable& tt, int b) {
+  int t = 0;
+  while (t + 1 < tt.n && tt.chunk0[t + 1] <= b) ++t;
+  return t;
+}
+
+__device__ __forceinline__ float block_sum_256(float v, float* red) {
+  v = wave_sum_f(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  const float r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g, const TensorTable tt,
+                                                    float* __restrict__ part) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const int t = table_find(tt, b);
+  const int c = b - tt.chunk0[t];
+  const int beg = c * UPD_CHUNK;
+  const int end = min(tt.numel[t], beg + UPD_CHUNK);
+  const float* gt = g + tt.off[t];
+  float s = 0.f;
+  for (int i = beg + threadIdx.x; i < end; i += 256) s = fmaf(gt[i], gt[i], s);
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) part[b] = s;
+}
+
+// clip_by_average_norm multiplier of tensor t: min(rsqrt(sum g^2) * n, 1/0.1)
+__device__ __forceinline__ float clip_factor(const TensorTable& tt, int t, const float* part) {
+  float ss = 0.f;
+  for (int b = tt.chunk0[t]; b < tt.chunk0[t + 1]; ++b) ss += part[b];
+  return fminf(rsqrtf(ss) * (float)tt.numel[t], 10.0f);
+}
+
+__global__ void __launch_bounds__(256) clip_kernel(float* __restrict__ g, const TensorTable tt,
+                                                   const float* __restrict__ part) {
+  const int b = blockIdx.x;
+  const int t = table_find(tt, b);
+  const int c = b - tt.chunk0[t];
+  const int beg = c * UPD_CHUNK;
+  const int end = min(tt.numel[t], beg + UPD_CHUNK);
+  const float f = clip_factor(tt, t, part);
+  float* gt = g + tt.off[t];
+  for (int i = beg + threadIdx.x; i < end; i += 256) gt[i] = (gt[i] * 0.1f) * f;
+}
+
+struct UpdateArgs {
+  float* p;
+  const float* g;
+  float* s0;
+  float* s1;
+  const float* clip_part;   // non-null: fuse clip_by_average_norm
+  float grad_scale;
+  float lr, one_minus_b1, one_minus_b2, eps, alpha;   // adam
+  float decay_c, momentum, rho, one_minus_rho;        // rms (decay_c = 1-decay), momentum, adadelta
+};
+
+template <int OPT>
+__global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const TensorTable tt) {
+  const int b = blockIdx.x;
+  const int t = table_find(tt, b);
+  const int c = b - tt.chunk0[t];
+  const int beg = c * UPD_CHUNK;
+  const int end = min(tt.numel[t], beg + UPD_CHUNK);
+  const long long o = tt.off[t];
+  const float f = a.clip_part ? clip_factor(tt, t, a.clip_part) : 0.f;
+  for (int i = beg + threadIdx.x; i < end; i += 256) {
+    const long long k = o + i;
+    float g = a.g[k];
+    g = a.clip_part ? (g * 0.1f) * f : g * a.grad_scale;
+    float p = a.p[k];
+    if constexpr (OPT == 0) {  // ApplyAdam
+      float m = a.s0[k], v = a.s1[k];
+      m += (g - m) * a.one_minus_b1;
+      v += (g * g - v) * a.one_minus_b2;
+      p -= (m * a.alpha) / (sqrtf(v) + a.eps);
+      a.s0[k] = m;
+      a.s1[k] = v;
+    } else if constexpr (OPT == 1) {  // ApplyGradientDescent
+      p -= g * a.lr;
+    } else if constexpr (OPT == 2) {  // ApplyAdagrad
+      float acc = a.s0[k] + g * g;
+      p -= g * a.lr * rsqrtf(acc);
+      a.s0[k] = acc;
+    } else if constexpr (OPT == 3) {  // ApplyAdadelta
+      float acc = a.s0[k] * a.rho + g * g * a.one_minus_rho;
+      float au = a.s1[k];
+      const float upd = sqrtf(au + a.eps) * rsqrtf(acc + a.eps) * g;
+      p -= upd * a.lr;
+      au = au * a.rho + upd * upd * a.one_minus_rho;
+      a.s0[k] = acc;
+      a.s1[k] = au;
+    } else if constexpr (OPT == 4) {  // ApplyMomentum (use_nesterov=False)
+      float acc = a.s0[k] * a.momentum + g;
+      p -= acc * a.lr;
+      a.s0[k] = acc;
+    } else {  // ApplyRMSProp
+      float ms = a.s0[k], mom = a.s1[k];
+      ms += (g * g - ms) * a.decay_c;
+      mom = mom * a.momentum + (g * a.lr) / sqrtf(ms + a.eps);
+      p -= mom;
+      a.s0[k] = ms;
+      a.s1[k] = mom;
+    }
+    a.p[k] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// numpy RandomState.choice(A, p=p) given its draw u:  cdf = cumsum(double(p)); cdf /= cdf[-1];
+// a = searchsorted(cdf, u, 'right').  flag bits: 1 non-finite p (train.py:381), 2 |sum-1| >
+// sqrt(eps_f32) ("probabilities do not sum to 1"), 4 negative p.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sample_kernel(const float* __restrict__ probs,
+                                                     const double* __restrict__ u, int B, int A,
+                                                     int64_t* __restrict__ actions, int* flag) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= B) return;
+  const float* pn = probs + (size_t)n * A;
+  double cdf[MAXA];
+  double cum = 0.0;
+  int bad = 0;
+  for (int k = 0; k < A; ++k) {
+    const float pk = pn[k];
+    if (!isfinite(pk)) bad |= 1;
+    if (pk < 0.f) bad |= 4;
+    cum += (double)pk;
+    cdf[k] = cum;
+  }
+  if (fabs(cum - 1.0) > 3.4526698300124393e-04) bad |= 2;
+  const double tot = cdf[A - 1];
+  const double un = u[n];
+  int64_t a = 0;
+  for (int k = 0; k < A; ++k) a += (cdf[k] / tot <= un) ? 1 : 0;
+  actions[n] = a;
+  if (bad && flag) atomicOr(flag, bad);
+}
+
+}  // namespace ba3c

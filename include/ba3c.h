@@ -1,0 +1,163 @@
+/*
+ * ba3c.h — C ABI of the MI355X-native BA3C learner/predictor hot path (libba3c.so).
+ *
+ * Plain pointers and sizes only: every device buffer is owned by the caller (the Python
+ * host allocates them with PyTorch-ROCm); the handle owns only static configuration and
+ * a few HIP events.  No call allocates device memory, none synchronises the stream except
+ * ba3c_probe_read, and none throws: every entry returns a BA3C_* status and
+ * ba3c_last_error() holds a thread-local message.  All device pointers must be 16-byte
+ * aligned.  `stream` is a hipStream_t (NULL = default stream).
+ *
+ * Each entry point replaces one piece of the reference TF-1.2 graph / runtime
+ * (paths relative to /root/reference/src):
+ *   ba3c_forward        OpenAIGym/train.py:164-299 for is_training=False (towerp0:
+ *                       'logitsT', 'pred_value'), served by OnlinePredictor._do_call
+ *                       tensorpack_cpu/tensorpack/predict/base.py:80-92 and
+ *                       MultiThreadAsyncPredictor predict/concurrency.py:172-219
+ *   ba3c_train_grads    OpenAIGym/train.py:164-327 forward + A3C loss and TF autodiff
+ *                       tensorpack_cpu/tensorpack/train/multigpu.py:85-86
+ *   ba3c_clip_grads     OpenAIGym/train.py:329-330 MapGradient(clip_by_average_norm(.,0.1)),
+ *                       applied per replica in train/base.py:206-217, multigpu.py:157
+ *   ba3c_apply_update   OpenAIGym/train.py:582-597 optimizer.apply_gradients
+ *                       (multigpu.py:194): Adam / RMSProp / GD / Momentum / Adagrad / Adadelta
+ *   ba3c_sample         OpenAIGym/train.py:382 np.random.choice(len(p), p=p) given its draw u
+ *   (gradient mean)     OpenAIGym/train.py:598-606 SyncReplicasOptimizer: the host
+ *                       all-reduces the clipped flat gradient buffer over RCCL between
+ *                       ba3c_clip_grads and ba3c_apply_update (grad_scale = 1/world).
+ */
+#ifndef BA3C_H
+#define BA3C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BA3C_OK 0
+#define BA3C_ERR_INVALID 1  /* bad argument / shape / config */
+#define BA3C_ERR_HIP 2      /* a HIP runtime call failed */
+
+/* optimizer ids (OpenAIGym/train.py:583-597, run_job.py -o choices) */
+#define BA3C_OPT_ADAM 0
+#define BA3C_OPT_GD 1
+#define BA3C_OPT_ADAGRAD 2
+#define BA3C_OPT_ADADELTA 3
+#define BA3C_OPT_MOMENTUM 4
+#define BA3C_OPT_RMS 5
+
+/* scalars written by ba3c_train_grads (double[BA3C_NUM_SCALARS]); names are the
+ * TfDictOp keys of train/multigpu.py:193-205 */
+#define BA3C_SC_COST 0
+#define BA3C_SC_POLICY_LOSS 1    /* policy_loss*128/B              train.py:311 */
+#define BA3C_SC_XENTROPY_LOSS 2  /* xentropy_loss*128/B*beta       train.py:315-316 */
+#define BA3C_SC_VALUE_LOSS 3     /* value_loss*128/B               train.py:320 */
+#define BA3C_SC_ADVANTAGE 4      /* mean(stop_grad(V)-R)           train.py:323 */
+#define BA3C_SC_PRED_REWARD 5    /* mean(V)                        train.py:321 */
+#define BA3C_SC_MAX_LOGIT 6      /* max(softmax)                   train.py:291 */
+#define BA3C_SC_ACTIVE_RELUS 7   /* sum count_nonzero(relu outs)   train.py:271 */
+#define BA3C_NUM_SCALARS 8
+
+/* kernel ids for the timing probe */
+#define BA3C_K_CONV0_FWD 0
+#define BA3C_K_CONV1_FWD 1
+#define BA3C_K_CONV2_FWD 2
+#define BA3C_K_CONV3_FWD 3
+#define BA3C_K_FC1_FWD 4
+#define BA3C_K_HEADS 5
+#define BA3C_K_FC1_DGRAD 6
+#define BA3C_K_CONV3_DGRAD 7
+#define BA3C_K_CONV2_DGRAD 8
+#define BA3C_K_CONV1_DGRAD 9
+#define BA3C_K_HEAD_WGRAD 10
+#define BA3C_K_FC1_WGRAD 11
+#define BA3C_K_CONV3_WGRAD 12
+#define BA3C_K_CONV2_WGRAD 13
+#define BA3C_K_CONV1_WGRAD 14
+#define BA3C_K_CONV0_WGRAD 15
+#define BA3C_K_WGRAD_REDUCE 16
+#define BA3C_K_CLIP 17
+#define BA3C_K_UPDATE 18
+#define BA3C_NUM_KERNELS 19
+
+typedef struct ba3c_handle ba3c_handle;
+
+/* Network geometry — the flag surface of OpenAIGym/parse.py:9-70 / run_job.py:13-48. */
+typedef struct ba3c_config {
+  int32_t max_batch;         /* largest B any call on this handle passes (workspace sizing) */
+  int32_t channels;          /* real input channels C = 4*--channels (4 or 12), train.py:95 */
+  int32_t fc_neurons;        /* --fc_neurons F (multiple of 4*fc_splits) */
+  int32_t fc_splits;         /* --fc_splits S  (train.py:216-229) */
+  int32_t num_actions;       /* A = env action count (train.py:122), 1..31 */
+  int32_t replace_with_conv; /* 1: --replace_with_conv True (default); 0: --use_normal_fc */
+  int32_t ps;                /* --ps: number of legacy FC splits (train.py:230-243) */
+} ba3c_config;
+
+/* Hyper-parameters of one optimizer apply. Power terms are the TF float32 variables
+ * beta1_power/beta2_power BEFORE this apply (beta^t at step t). */
+typedef struct ba3c_opt_params {
+  float lr, beta1, beta2, epsilon;    /* Adam (train.py:584) */
+  float beta1_power, beta2_power;     /* Adam bias-correction state */
+  float decay, momentum;              /* RMSProp (TF defaults 0.9 / 0.0), Momentum 0.9 */
+  float rho;                          /* Adadelta (0.95) */
+} ba3c_opt_params;
+
+int ba3c_create(const ba3c_config* cfg, ba3c_handle** out);
+void ba3c_destroy(ba3c_handle* h);
+const char* ba3c_last_error(void);
+int ba3c_version(void);
+
+/* Flat parameter layout shared by params / grads / optimizer slots.  Tensor i is
+ * name (checkpoint key, e.g. "conv0/W"), at float offset `offset`, `numel` elements in
+ * TF layout (HWIO conv, [in,out] FC).  Offsets are 64-float aligned; gaps are zero. */
+int ba3c_num_tensors(const ba3c_handle* h);
+int ba3c_tensor_info(const ba3c_handle* h, int32_t i, const char** name, int64_t* offset,
+                     int64_t* numel, int32_t shape[4], int32_t* ndim);
+int64_t ba3c_flat_size(const ba3c_handle* h);
+/* Bytes of scratch device memory a call with batch B needs (train=1: ba3c_train_grads). */
+size_t ba3c_workspace_size(const ba3c_handle* h, int32_t batch, int32_t train);
+
+/* Predictor: one forward of B uint8 [B,84,84,C] states.  probs = softmax(policy)
+ * ('logits', train.py:288), probsT = softmax(policy*explore_factor) ('logitsT', :299),
+ * value = 'pred_value' [B].  Any output pointer may be NULL. */
+int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                 int32_t batch, float explore_factor, void* workspace, float* probs,
+                 float* probsT, float* value);
+
+/* Learner: forward + A3C loss + backward for one tower.  Writes RAW (unclipped) gradients
+ * of every tensor into `grads` (flat layout, fully overwritten incl. gaps) and
+ * BA3C_NUM_SCALARS doubles into `scalars` (device memory, may be NULL).
+ * action: int64 [B] in [0,A); futurereward: fp32 [B]. */
+int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                     const int64_t* action, const float* futurereward, int32_t batch,
+                     float entropy_beta, void* workspace, float* grads, double* scalars);
+
+/* Per-tensor tf.clip_by_average_norm(g, 0.1) in place (n = graph numel incl. padding). */
+int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace);
+
+/* One optimizer apply over the flat buffers: g_eff = grads*grad_scale (1/world after an
+ * all-reduce-sum), or, with fuse_clip=1, clip_by_average_norm(grads) fused in (single
+ * replica).  slot0/slot1: Adam m/v, RMS ms/mom, Adagrad accum, Adadelta accum/accum_update,
+ * Momentum accum; unused slots may be NULL. */
+int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
+                      const float* grads, float* slot0, float* slot1,
+                      const ba3c_opt_params* hp, float grad_scale, int32_t fuse_clip,
+                      void* workspace);
+
+/* Action sampling: actions[i] = #{k : cdf_i[k] <= u[i]} with cdf_i = cumsum(double(p_i))
+ * / cdf_i[A-1]  (numpy RandomState.choice).  nonfinite (device int32, may be NULL) is
+ * set to 1 if any probability is not finite (train.py:381 assert). */
+int ba3c_sample(void* stream, const float* probs, const double* u, int32_t batch,
+                int32_t num_actions, int64_t* actions, int32_t* nonfinite);
+
+/* Timing probe: bracket every launch of kernel `kernel_id` with HIP events (on the stream
+ * it is launched on) until disabled (kernel_id = -1).  ba3c_probe_read synchronises the
+ * recorded events and returns the summed milliseconds and launch count since enabling. */
+int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
+int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BA3C_H */
