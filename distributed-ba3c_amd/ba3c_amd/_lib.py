@@ -63,6 +63,8 @@ def load():
                                    ctypes.POINTER(i64), ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "ba3c_flat_size": (i64, [P]),
         "ba3c_workspace_size": (ctypes.c_size_t, [P, i32, i32]),
+        "ba3c_workspace_tensor": (i32, [P, i32, i32, ctypes.c_char_p, ctypes.POINTER(i64),
+                                        ctypes.POINTER(i64)]),
         "ba3c_forward": (i32, [P, P, P, P, i32, f32, P, P, P, P]),
         "ba3c_train_grads": (i32, [P, P, P, P, P, P, i32, f32, P, P, P]),
         "ba3c_clip_grads": (i32, [P, P, P, P]),

@@ -105,6 +105,16 @@ class Ba3cEngine(object):
             self.ws_fwd = torch.empty(n, dtype=torch.uint8, device=self.device)
         return self.ws_fwd
 
+    def workspace_tensor(self, name, batch, train=True):
+        """View of an intermediate of the last call with this batch (tests / debugging)."""
+        off, nb = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self.lib.ba3c_workspace_tensor(self.h, batch, 1 if train else 0,
+                                                  name.encode(), ctypes.byref(off),
+                                                  ctypes.byref(nb)))
+        ws = self._workspace(train)
+        raw = ws[off.value:off.value + nb.value]
+        return raw if name.startswith("c") else raw.view(torch.float32)
+
     def _check_state(self, state):
         assert state.dtype == torch.uint8 and state.is_cuda and state.is_contiguous(), \
             "state must be a contiguous uint8 device tensor [B,84,84,C]"

@@ -121,7 +121,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   char* p = static_cast<char*>(base);
   size_t off = 0;
   auto take = [&](size_t bytes) -> char* {
-    char* r = p ? p + off : nullptr;
+    char* r = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(p) + off);  // p may be 0: offsets
     off += align256(bytes);
     return r;
   };
@@ -132,7 +132,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   w.p2 = (float*)take(Bz * P2 * 4);
   w.a3 = (float*)take(Bz * A3 * 4);
   w.h = (float*)take(Bz * F * 4);
-  w.relu = (unsigned long long*)take(64);
+  w.relu = (unsigned long long*)take(RELU_SLOTS * 8);
   if (train) {
     w.c0 = (uint8_t*)take(Bz * P0);
     w.c1 = (uint8_t*)take(Bz * P1);
@@ -470,6 +470,32 @@ int ba3c_tensor_info(const ba3c_handle* h, int32_t i, const char** name, int64_t
 
 int64_t ba3c_flat_size(const ba3c_handle* h) { return h ? h->flat : 0; }
 
+int ba3c_workspace_tensor(const ba3c_handle* h, int32_t batch, int32_t train, const char* name,
+                          int64_t* offset_bytes, int64_t* bytes) {
+  if (!h || !name || batch < 1) return fail(BA3C_ERR_INVALID, "bad argument");
+  Workspace w = carve(h, nullptr, batch, train != 0);
+  // carve() with a null base returns offsets as pointers from 0
+  const size_t Bz = (size_t)batch;
+  const int F = h->cfg.fc_neurons;
+  struct Item { const char* n; const void* p; size_t b; };
+  const Item items[] = {
+      {"p0", w.p0, Bz * P0 * 4}, {"p1", w.p1, Bz * P1 * 4}, {"p2", w.p2, Bz * P2 * 4},
+      {"a3", w.a3, Bz * A3 * 4}, {"h", w.h, Bz * F * 4},     {"c0", w.c0, Bz * P0},
+      {"c1", w.c1, Bz * P1},     {"c2", w.c2, Bz * P2},     {"dh", w.dh, Bz * F * 4},
+      {"dy3", w.dy3, Bz * A3 * 4}, {"dp2", w.dp2, Bz * P2 * 4}, {"dp1", w.dp1, Bz * P1 * 4},
+      {"dp0", w.dp0, Bz * P0 * 4}};
+  for (const Item& it : items) {
+    if (std::strcmp(it.n, name) == 0) {
+      if (!train && it.n[0] != 'p' && it.n[0] != 'a' && it.n[0] != 'h')
+        return fail(BA3C_ERR_INVALID, "tensor only exists in the training workspace");
+      if (offset_bytes) *offset_bytes = (int64_t)reinterpret_cast<uintptr_t>(it.p);
+      if (bytes) *bytes = (int64_t)it.b;
+      return BA3C_OK;
+    }
+  }
+  return fail(BA3C_ERR_INVALID, std::string("unknown workspace tensor ") + name);
+}
+
 size_t ba3c_workspace_size(const ba3c_handle* h, int32_t batch, int32_t train) {
   if (!h || batch < 1) return 0;
   return carve(h, nullptr, batch, train != 0).bytes;
@@ -500,7 +526,7 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
   hipStream_t s = static_cast<hipStream_t>(stream);
   Workspace w = carve(h, workspace, batch, true);
   HIP_TRY(hipMemsetAsync(grads, 0, (size_t)h->flat * 4, s));
-  HIP_TRY(hipMemsetAsync(w.relu, 0, 8, s));
+  HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_SLOTS * 8, s));
   int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, true)
                                : run_forward<12>(h, s, params, state, batch, w, true);
   if (r != BA3C_OK) return r;

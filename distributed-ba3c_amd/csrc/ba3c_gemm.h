@@ -181,6 +181,12 @@ __device__ __forceinline__ float wave_sum_f(float v) {
   return v;
 }
 
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __device__ __forceinline__ float wave_max_f(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

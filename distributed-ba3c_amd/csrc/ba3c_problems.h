@@ -16,6 +16,18 @@ __device__ __forceinline__ float4 u8x4_to_f4(uint32_t v) {
                      (float)(v >> 24));
 }
 
+// count_nonzero of ReLU outputs (train.py:271): one integer add per wave, spread over
+// RELU_SLOTS counters so 10^5 waves do not serialise on one address (summed by the scalars
+// kernel; integer adds are exact in any order).
+constexpr int RELU_SLOTS = 1024;
+__device__ __forceinline__ void relu_count_add(unsigned long long* slots, unsigned long long pos, int lane) {
+  pos = wave_sum_u64(pos);
+  if (lane == 0 && pos) {
+    const unsigned slot = (blockIdx.x * 4u + (threadIdx.x >> 6) + blockIdx.y * 977u) & (RELU_SLOTS - 1);
+    atomicAdd(slots + slot, pos);
+  }
+}
+
 // dY at conv-output position (y, x) from pooled grad dP and argmax codes.
 template <int PW, int COUT>
 __device__ __forceinline__ float4 unpool4(const float* __restrict__ dP, const uint8_t* __restrict__ code,
@@ -128,10 +140,7 @@ struct ConvFwd {
           }
         }
       }
-    if (relu_count) {
-      pos = wave_sum_u64(pos);
-      if (lane == 0 && pos) atomicAdd(relu_count, pos);
-    }
+    if (relu_count) relu_count_add(relu_count, pos, lane);
   }
 };
 
@@ -318,10 +327,7 @@ struct FcFwd {
           if (m < M && col < N) h[(size_t)m * N + col] = v;
         }
       }
-    if (legacy && relu_count) {
-      pos = wave_sum_u64(pos);
-      if (lane == 0 && pos) atomicAdd(relu_count, pos);
-    }
+    if (legacy && relu_count) relu_count_add(relu_count, pos, lane);
   }
 };
 

@@ -3,7 +3,7 @@
 // reduction of weight gradients, tf.clip_by_average_norm (train.py:329-330), the TF-1.2
 // optimizer applies (train.py:582-597) and numpy-exact action sampling (train.py:382).
 #pragma once
-#include "ba3c_gemm.h"
+#include "ba3c_problems.h"
 
 namespace ba3c {
 
@@ -38,125 +38,131 @@ struct HeadsArgs {
   float beta, explore, invB;
 };
 
+// The per-sample head arithmetic runs in fp64: the softmax gradient
+// p_k (g_k - sum_j p_j g_j) cancels catastrophically when the policy saturates, and fp64 here
+// costs nothing measurable (F*(A+1) FMAs per sample) while keeping the fp32 stored results
+// within rounding of the exact values.
 __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= p.B) return;
   const int A = p.A;
-  float acc[MAXA];
+  double acc[MAXA];
 #pragma unroll
-  for (int a = 0; a < MAXA; ++a) acc[a] = 0.f;
-  float accv = 0.f;
+  for (int a = 0; a < MAXA; ++a) acc[a] = 0.0;
+  double accv = 0.0;
   const float* hn = p.h + (size_t)n * p.F;
   for (int f = lane; f < p.F; f += 64) {
-    const float hv = hn[f];
+    const double hv = hn[f];
     const float* wr = p.piW + (size_t)f * A;
 #pragma unroll
     for (int a = 0; a < MAXA; ++a)
-      if (a < A) acc[a] = fmaf(hv, wr[a], acc[a]);
-    accv = fmaf(hv, p.vW[f], accv);
+      if (a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
+    accv = fma(hv, (double)p.vW[f], accv);
   }
-  float z[MAXA];
-  float zmax = -INFINITY;
+  double z[MAXA];
+  double zmax = -INFINITY;
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
     if (a < A) {
-      z[a] = wave_sum_f(acc[a]) + p.pib[a];
-      zmax = fmaxf(zmax, z[a]);
+      z[a] = wave_sum_d(acc[a]) + (double)p.pib[a];
+      zmax = fmax(zmax, z[a]);
     } else {
-      z[a] = 0.f;
+      z[a] = 0.0;
     }
   }
-  const float V = wave_sum_f(accv) + p.vb[0];
+  const double V = wave_sum_d(accv) + (double)p.vb[0];
   // softmax(z)  (tf.nn.softmax: exp(z - max) / sum)
-  float pr[MAXA];
-  float s = 0.f;
+  double pr[MAXA];
+  double s = 0.0;
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
-    pr[a] = a < A ? expf(z[a] - zmax) : 0.f;
+    pr[a] = a < A ? exp(z[a] - zmax) : 0.0;
     s += pr[a];
   }
-  float pmax = 0.f;
+  double pmax = 0.0;
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
-    pr[a] = a < A ? pr[a] / s : 0.f;
-    pmax = fmaxf(pmax, pr[a]);
+    pr[a] = a < A ? pr[a] / s : 0.0;
+    pmax = fmax(pmax, pr[a]);
   }
   if (p.probsT) {
-    float zt[MAXA];
-    float ztmax = -INFINITY, st = 0.f;
+    double zt[MAXA];
+    double ztmax = -INFINITY, st = 0.0;
+    const double ex = (double)p.explore;
 #pragma unroll
     for (int a = 0; a < MAXA; ++a) {
-      zt[a] = z[a] * p.explore;
-      if (a < A) ztmax = fmaxf(ztmax, zt[a]);
+      zt[a] = z[a] * ex;
+      if (a < A) ztmax = fmax(ztmax, zt[a]);
     }
 #pragma unroll
     for (int a = 0; a < MAXA; ++a) {
-      zt[a] = a < A ? expf(zt[a] - ztmax) : 0.f;
+      zt[a] = a < A ? exp(zt[a] - ztmax) : 0.0;
       st += zt[a];
     }
 #pragma unroll
     for (int a = 0; a < MAXA; ++a)
-      if (a < A && lane == a) p.probsT[(size_t)n * A + a] = zt[a] / st;
+      if (a < A && lane == a) p.probsT[(size_t)n * A + a] = (float)(zt[a] / st);
   }
   if (p.probs) {
 #pragma unroll
     for (int a = 0; a < MAXA; ++a)
-      if (a < A && lane == a) p.probs[(size_t)n * A + a] = pr[a];
+      if (a < A && lane == a) p.probs[(size_t)n * A + a] = (float)pr[a];
   }
-  if (p.value && lane == 0) p.value[n] = V;
+  if (p.value && lane == 0) p.value[n] = (float)V;
   if (!p.train) return;
 
-  const float Rn = p.R[n];
+  const double Rn = p.R[n];
   const int act = (int)p.action[n];
-  const float adv = V - Rn;
-  float gp[MAXA];
-  float lpa = 0.f, xent = 0.f, sgp = 0.f;
+  const double adv = V - Rn;
+  const double beta = (double)p.beta, invB = 1.0 / (double)p.B;
+  double gp[MAXA];
+  double lpa = 0.0, xent = 0.0, sgp = 0.0;
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
     if (a < A) {
-      const float pe = pr[a] + 1e-6f;
-      const float lp = logf(pe);
+      const double pe = pr[a] + 1e-6;
+      const double lp = log(pe);
       xent += pr[a] * lp;
       if (a == act) lpa = lp;
-      gp[a] = ((a == act ? adv / pe : 0.f) + p.beta * (lp + pr[a] / pe)) * p.invB;
+      gp[a] = ((a == act ? adv / pe : 0.0) + beta * (lp + pr[a] / pe)) * invB;
       sgp += gp[a] * pr[a];
     } else {
-      gp[a] = 0.f;
+      gp[a] = 0.0;
     }
   }
-  float dz[MAXA];
+  double dz[MAXA];
 #pragma unroll
-  for (int a = 0; a < MAXA; ++a) dz[a] = a < A ? pr[a] * (gp[a] - sgp) : 0.f;
-  const float dV = (V - Rn) * p.invB;
+  for (int a = 0; a < MAXA; ++a) dz[a] = a < A ? pr[a] * (gp[a] - sgp) : 0.0;
+  const double dV = (V - Rn) * invB;
   // [dz | dV | 0...] row for the head weight-gradient product
   {
-    float mine = 0.f;
+    double mine = 0.0;
 #pragma unroll
     for (int a = 0; a < MAXA; ++a)
       if (lane == a) mine = dz[a];
     if (lane == A) mine = dV;
-    if (lane < MAXA) p.dzv[(size_t)n * MAXA + lane] = mine;
+    if (lane < MAXA) p.dzv[(size_t)n * MAXA + lane] = (float)mine;
   }
   float* dhn = p.dh + (size_t)n * p.F;
   for (int f = lane; f < p.F; f += 64) {
     const float* wr = p.piW + (size_t)f * A;
-    float g = dV * p.vW[f];
+    double g = dV * (double)p.vW[f];
 #pragma unroll
     for (int a = 0; a < MAXA; ++a)
-      if (a < A) g = fmaf(dz[a], wr[a], g);
-    if (p.legacy && !(hn[f] > 0.f)) g = 0.f;
-    dhn[f] = g;
+      if (a < A) g = fma(dz[a], (double)wr[a], g);
+    if (p.legacy && !(hn[f] > 0.f)) g = 0.0;
+    dhn[f] = (float)g;
   }
   if (lane < NTERMS) {
-    float t = 0.f;
+    double t = 0.0;
     t = lane == 0 ? lpa * adv : t;
     t = lane == 1 ? xent : t;
     t = lane == 2 ? (V - Rn) * (V - Rn) : t;
     t = lane == 3 ? adv : t;
     t = lane == 4 ? V : t;
     t = lane == 5 ? pmax : t;
-    p.terms[(size_t)n * NTERMS + lane] = t;
+    p.terms[(size_t)n * NTERMS + lane] = (float)t;
   }
 }
 
@@ -179,7 +185,19 @@ __global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B,
   }
   for (int i = 0; i < 5; ++i) red[i][t] = s[i];
   red[5][t] = mx;
+  __shared__ unsigned long long rsum[256];
+  unsigned long long rc = 0;
+  if (relu_count)
+    for (int i = t; i < RELU_SLOTS; i += 256) rc += relu_count[i];
+  rsum[t] = rc;
   __syncthreads();
+  if (t == 0) {
+    unsigned long long tot = 0;
+    for (int i = 0; i < 256; ++i) tot += rsum[i];
+    rsum[0] = tot;
+  }
+  __syncthreads();
+  const unsigned long long relu_total = rsum[0];
   for (int w = 128; w >= 1; w >>= 1) {
     if (t < w) {
       for (int i = 0; i < 5; ++i) red[i][t] += red[i][t + w];
@@ -197,7 +215,7 @@ __global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B,
     out[4] = red[3][0] / Bd;
     out[5] = red[4][0] / Bd;
     out[6] = red[5][0];
-    out[7] = relu_count ? (double)(*relu_count) : 0.0;
+    out[7] = (double)relu_total;
   }
 }
 

@@ -117,6 +117,12 @@ int ba3c_tensor_info(const ba3c_handle* h, int32_t i, const char** name, int64_t
 int64_t ba3c_flat_size(const ba3c_handle* h);
 /* Bytes of scratch device memory a call with batch B needs (train=1: ba3c_train_grads). */
 size_t ba3c_workspace_size(const ba3c_handle* h, int32_t batch, int32_t train);
+/* Introspection of the workspace a call with batch B carved (for tests / debugging): byte
+ * offset and size of an intermediate — "p0","p1","p2" pooled maps [B,H,W,C] fp32, "c0".."c2"
+ * argmax codes (uint8, 0..3 = first max of the 2x2 window, 255 = max <= 0), "a3" [B,1600],
+ * "h" [B,F], and in training "dh","dy3","dp2","dp1","dp0" gradients. */
+int ba3c_workspace_tensor(const ba3c_handle* h, int32_t batch, int32_t train, const char* name,
+                          int64_t* offset_bytes, int64_t* bytes);
 
 /* Predictor: one forward of B uint8 [B,84,84,C] states.  probs = softmax(policy)
  * ('logits', train.py:288), probsT = softmax(policy*explore_factor) ('logitsT', :299),

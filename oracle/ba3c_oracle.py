@@ -324,25 +324,42 @@ def _backward_from_heads(params, t, cfg, dz, dV):
             g["fc1_%d/b" % i] = sl.sum(axis=0)
             dflat += sl @ params["fc1_%d/W" % i].T
     Bn = flat.shape[0]
-    da3 = dflat.reshape(Bn, 5, 5, 64) * (t["a3"] > 0)                      # ReluGrad (A.2)
+    forced = t.get("forced")
+
+    def pool_back(dp, layer, hw, act):
+        if forced is None:
+            return maxpool2x2_backward(dp, t["c%d" % layer], hw) * (act > 0)
+        # the checked side's own discrete decisions: code 255 = window max <= 0 (no gradient)
+        c = forced["c%d" % layer]
+        return maxpool2x2_backward(np.where(c == 255, 0, dp), np.where(c == 255, 0, c), hw)
+
+    mask3 = (t["a3"] > 0) if forced is None else forced["a3_mask"]
+    da3 = dflat.reshape(Bn, 5, 5, 64) * mask3                               # ReluGrad (A.2)
     g["conv3/W"] = conv2d_valid_wgrad(t["p2"], da3, (3, 3))
     dp2 = conv2d_valid_dgrad(da3, params["conv3/W"], (7, 7))
-    da2 = maxpool2x2_backward(dp2, t["c2"], (14, 14)) * (t["a2"] > 0)
+    da2 = pool_back(dp2, 2, (14, 14), t["a2"])
     g["conv2/W"] = conv2d_valid_wgrad(t["p1"], da2, (5, 5))
     dp1 = conv2d_valid_dgrad(da2, params["conv2/W"], (18, 18))
-    da1 = maxpool2x2_backward(dp1, t["c1"], (36, 36)) * (t["a1"] > 0)
+    da1 = pool_back(dp1, 1, (36, 36), t["a1"])
     g["conv1/W"] = conv2d_valid_wgrad(t["p0"], da1, (5, 5))
     dp0 = conv2d_valid_dgrad(da1, params["conv1/W"], (40, 40))
-    da0 = maxpool2x2_backward(dp0, t["c0"], (80, 80)) * (t["a0"] > 0)
+    da0 = pool_back(dp0, 0, (80, 80), t["a0"])
     g["conv0/W"] = conv2d_valid_wgrad(t["x"], da0, (5, 5))                  # incl. padded ch.
     t.update(dz=dz, dV=dV, dh=dh, da3=da3, dp2=dp2, dp1=dp1, dp0=dp0)
     return g
 
 
-def loss_and_grads(params, state, action, futurereward, cfg, entropy_beta=0.01):
-    """One tower's forward + loss + raw gradients (before the gradient processor)."""
+def loss_and_grads(params, state, action, futurereward, cfg, entropy_beta=0.01, forced=None):
+    """One tower's forward + loss + raw gradients (before the gradient processor).
+
+    `forced` (tests only) = {'c0','c1','c2': uint8 argmax codes with 255 for max<=0,
+    'a3_mask': bool} replaces the oracle's own max-pool / ReLU decisions in the backward pass,
+    so an fp32 implementation can be compared on arithmetic alone when a near-tie or a
+    pre-activation within rounding of zero resolves differently in fp32 and fp64."""
     t, scalars = build_graph_cost(params, state, action, futurereward, cfg, entropy_beta)
     t["R"] = futurereward.astype(params["conv0/W"].dtype)
+    if forced is not None:
+        t["forced"] = forced
     grads = backward(params, t, cfg, entropy_beta)
     return t, scalars, grads
 

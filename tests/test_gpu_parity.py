@@ -55,6 +55,22 @@ def as64(params):
     return {k: v.astype(np.float64) for k, v in params.items()}
 
 
+def gpu_decisions(eng, B):
+    """The HIP path's own max-pool argmax codes and conv3 ReLU mask of the last train call."""
+    shapes = {0: (B, 40, 40, 32), 1: (B, 18, 18, 32), 2: (B, 7, 7, 64)}
+    codes = [eng.workspace_tensor("c%d" % l, B).cpu().numpy().reshape(shapes[l]) for l in range(3)]
+    a3 = eng.workspace_tensor("a3", B).cpu().numpy().reshape(B, 5, 5, 64)
+    forced = {"c0": codes[0], "c1": codes[1], "c2": codes[2], "a3_mask": a3 > 0}
+    return forced, codes
+
+
+def value_err(v_gpu, t, params):
+    """|dV| relative to the magnitude of the summed terms of V = h.Wv + b (normwise: an fp32
+    evaluation of a sum with cancellation is only accurate to eps * sum|terms|)."""
+    scale = (np.abs(t["h"]) @ np.abs(params["fc-v/W"].astype(np.float64)))[:, 0] + abs(float(params["fc-v/b"][0]))
+    return float(np.abs(np.asarray(v_gpu, np.float64) - t["pred_value"]).max() / scale.max())
+
+
 CONFIGS = [
     dict(A=4, C=4, F=128, S=4),                 # BASELINE cfg2 geometry
     dict(A=6, C=12, F=512, S=1),                # RGB x4 frames, default F
@@ -73,7 +89,7 @@ def test_forward_matches_oracle(cfgk, B):
     torch.cuda.synchronize()
     assert rel(probs.cpu().numpy(), t["logits"]) < FWD_TOL
     assert rel(probsT.cpu().numpy(), t["logitsT"]) < FWD_TOL
-    assert rel(value.cpu().numpy(), t["pred_value"]) < FWD_TOL
+    assert value_err(value.cpu().numpy(), t, params) < FWD_TOL
 
 
 @pytest.mark.parametrize("cfgk", CONFIGS)
@@ -83,8 +99,15 @@ def test_gradients_and_scalars_match_oracle(cfgk, B):
     eng = engine(**cfgk)
     eng.load_params(params)
     sc = eng.train_grads(dev(state), dev(action), dev(R), entropy_beta=0.01)
-    t, osc, g = O.loss_and_grads(as64(params), state, action, R.astype(np.float64), cfg)
     got = eng.state_dict(eng.grads)
+    forced, codes = gpu_decisions(eng, B)
+    t, osc, g = O.loss_and_grads(as64(params), state, action, R.astype(np.float64), cfg,
+                                 forced=forced)
+    # discrete decisions (first-max argmax, ReLU sign) may differ only on fp32 near-ties
+    for layer in range(3):
+        own = np.where(t["p%d" % layer] > 0, t["c%d" % layer], 255)
+        assert np.mean(own != codes[layer]) < 1e-4, layer
+    assert np.mean((t["a3"] > 0) != forced["a3_mask"]) < 1e-4
     for k in g:
         e = rel(got[k], g[k])
         assert e < GRAD_TOL, (k, e)
@@ -95,7 +118,8 @@ def test_gradients_and_scalars_match_oracle(cfgk, B):
     for i, name in enumerate(SCALAR_NAMES):
         ref = float(osc[name])
         assert abs(s[i] - ref) <= 1e-4 * max(1.0, abs(ref)), (name, s[i], ref)
-    assert int(s[7]) == osc["active_relus"]
+    # count_nonzero of ReLU outputs: a pre-activation within fp32 rounding of 0 may flip
+    assert abs(int(s[7]) - osc["active_relus"]) <= max(2, 1e-5 * osc["active_relus"])
 
 
 def test_clip_kernel_matches_tf_formula():
@@ -121,7 +145,9 @@ def test_optimizer_kernel_matches_tf_functor(opt):
     o = make_optimizer(opt, 1e-3, beta1=0.8, beta2=0.75, epsilon=1e-8)
     ref_p = {k: v.copy() for k, v in params.items()}
     ref_s = O.init_slots(ref_p, opt, beta1=0.8, beta2=0.75)
+    upd_scale = {k: 0.0 for k in ref_p}
     for step in range(3):
+        prev = {k: v.astype(np.float64) for k, v in ref_p.items()}
         eng.train_grads(dev(state), dev(action), dev(R))
         g = {k: O.clip_by_average_norm(v) for k, v in eng.state_dict(eng.grads).items()}
         o.apply_gradients(eng, fuse_clip=True)
@@ -147,12 +173,14 @@ def test_optimizer_kernel_matches_tf_functor(opt):
             ref_s["beta2_power"] = np.float32(ref_s["beta2_power"] * np.float32(0.75))
         got = eng.state_dict()
         for k in ref_p:
-            d_got = got[k].astype(np.float64) - params[k]
-            d_ref = ref_p[k].astype(np.float64) - params[k]
-            if np.abs(d_ref).max() == 0:
-                assert np.abs(d_got).max() == 0, k
-                continue
-            assert rel(d_got, d_ref) < GRAD_TOL, (opt, step, k, rel(d_got, d_ref))
+            # both sides round p to fp32 after the same functor arithmetic: allow the update
+            # tolerance (relative to the largest per-step update so far) plus a few ulps of p
+            upd_scale[k] = max(upd_scale[k], float(np.abs(ref_p[k] - prev[k]).max()))
+            err = np.abs(got[k].astype(np.float64) - ref_p[k])
+            lim = GRAD_TOL * upd_scale[k] + 4 * np.spacing(np.abs(ref_p[k]).astype(np.float32))
+            bad = err > lim
+            assert not bad.any(), (opt, step, k, got[k][bad][:4], ref_p[k][bad][:4],
+                                   params[k][bad][:4], g[k][bad][:4])
 
 
 def test_end_to_end_adam_step_vs_oracle_train_step():
@@ -205,14 +233,17 @@ def test_sampling_flags_nonfinite_and_bad_sum():
 def test_maxpool_ties_route_gradient_to_first_max():
     """Constant frames make every conv0 window tie: the gradient must go to the FIRST max of
     each window (TF's MaxPoolGrad), exactly as the oracle routes it."""
-    params, _, action, R, cfg = case(5, 4, wscale=2.0)
+    params, _, action, R, cfg = case(5, 4, wscale=1.0)
     params["conv0/W"] = np.abs(params["conv0/W"])          # positive outputs everywhere
     state = np.full((4, 84, 84, 4), 200, np.uint8)
     state[1, :, ::2] = 17                                   # ties along rows only
     eng = engine()
     eng.load_params(params)
     eng.train_grads(dev(state), dev(action), dev(R))
-    _, _, g = O.loss_and_grads(as64(params), state, action, R.astype(np.float64), cfg)
+    t, _, g = O.loss_and_grads(as64(params), state, action, R.astype(np.float64), cfg)
     got = eng.state_dict(eng.grads)
+    _, codes = gpu_decisions(eng, 4)
+    for layer in range(3):      # identical routing decisions on exact ties
+        np.testing.assert_array_equal(codes[layer], np.where(t["p%d" % layer] > 0, t["c%d" % layer], 255))
     for k in g:
         assert rel(got[k], g[k]) < GRAD_TOL, k
