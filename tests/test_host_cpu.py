@@ -1,0 +1,163 @@
+"""Host logic on CPU (no GPU): the trainer / SyncReplicasOptimizer aggregation over a
+world-size-2 gloo group, the TF optimizer state bookkeeping and the flag surface.
+
+The compute engine here is a test double backed by the oracle (test infrastructure); the
+product path (Ba3cEngine) refuses to run without the HIP library and a GPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ba3c_oracle as O
+
+CFG = {"fc_neurons": 16, "fc_splits": 2}
+
+
+class OracleEngine(object):
+    """Same surface as ba3c_amd.engine.Ba3cEngine, computing with the oracle on the CPU."""
+
+    def __init__(self, params):
+        self.names = list(params)
+        self.shapes = {k: v.shape for k, v in params.items()}
+        self.offs = {}
+        off = 0
+        for k in self.names:
+            self.offs[k] = off
+            off += params[k].size
+        self.flat_size = off
+        self.params = torch.from_numpy(np.concatenate([params[k].reshape(-1) for k in self.names]))
+        self.grads = torch.zeros_like(self.params)
+        self.scalars = torch.zeros(8, dtype=torch.float64)
+        self.device = torch.device("cpu")
+        self.num_actions = 4
+
+    @property
+    def tensor_names(self):
+        return self.names
+
+    def state_dict(self, flat=None):
+        flat = (self.params if flat is None else flat).numpy()
+        return {k: flat[self.offs[k]:self.offs[k] + int(np.prod(self.shapes[k]))].reshape(self.shapes[k]).copy()
+                for k in self.names}
+
+    def zeros_like_flat(self, fill=0.0):
+        return torch.full((self.flat_size,), fill, dtype=torch.float32)
+
+    def train_grads(self, state, action, R, entropy_beta=0.01, grads=None):
+        _, sc, g = O.loss_and_grads(self.state_dict(), state.numpy(), action.numpy(), R.numpy(), CFG)
+        self.grads.copy_(torch.from_numpy(np.concatenate([g[k].reshape(-1) for k in self.names])))
+        self.scalars[0] = float(sc["cost"])
+        return self.scalars
+
+    def clip_grads(self, grads=None):
+        g = self.state_dict(self.grads)
+        self.grads.copy_(torch.from_numpy(np.concatenate(
+            [O.clip_by_average_norm(g[k]).reshape(-1) for k in self.names])))
+
+    def apply_update(self, opt, slot0, slot1, hp, grad_scale=1.0, fuse_clip=False, grads=None):
+        assert opt == "adam"
+        if fuse_clip:
+            self.clip_grads()
+            grad_scale = 1.0
+        g = self.state_dict(self.grads)
+        p, m, v = self.state_dict(), self.state_dict(slot0), self.state_dict(slot1)
+        for k in self.names:
+            gk = (g[k] * np.float32(grad_scale)).astype(np.float32)
+            p[k], m[k], v[k] = O.apply_adam(p[k], gk, m[k], v[k], hp["lr"], hp["beta1"], hp["beta2"],
+                                            hp["epsilon"], hp["beta1_power"], hp["beta2_power"])
+        for buf, d in ((self.params, p), (slot0, m), (slot1, v)):
+            buf.copy_(torch.from_numpy(np.concatenate([d[k].reshape(-1) for k in self.names])))
+
+
+def _batch(seed, B=2):
+    rs = np.random.RandomState(seed)
+    return (rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8),
+            rs.randint(0, 4, size=B).astype(np.int64), rs.normal(size=B).astype(np.float32))
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ba3c_amd.model import Model
+    from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
+    from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
+    params = O.init_params(16, 2, 4, seed=0, dtype=np.float32)
+    eng = OracleEngine(params)
+    model = Model(num_actions=4, fc_neurons=16, fc_splits=2, batch_size=2, engine=eng)
+    opt = SyncReplicasOptimizer(AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), world, world)
+    tr = Ba3cTrainer(TrainConfig(model=model, optimizer=opt))
+    for step in range(2):
+        s, a, r = _batch(10 * step + rank)
+        tr.train_step(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(r))
+    out[rank] = eng.params.numpy().copy()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sync_replicas_world2_gloo_matches_oracle_sync_step():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    # replicas stay bit-identical
+    np.testing.assert_array_equal(out[0], out[1])
+    # and equal the oracle's SyncReplicas step: mean of per-replica clipped grads, one Adam
+    params = O.init_params(16, 2, 4, seed=0, dtype=np.float32)
+    slots = O.init_slots(params, "adam", 0.8, 0.75)
+    for step in range(2):
+        batches = [_batch(10 * step + r) for r in range(world)]
+        params, slots, _, _ = O.train_step(params, slots, step + 1, batches, CFG, lr=1e-3,
+                                           beta1=0.8, beta2=0.75, eps=1e-8)
+    ref = np.concatenate([params[k].reshape(-1) for k in params])
+    np.testing.assert_allclose(out[0], ref, rtol=2e-6, atol=1e-9)
+
+
+def test_sync_replicas_rejects_backup_workers():
+    from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
+    with pytest.raises(ValueError):
+        SyncReplicasOptimizer(AdamOptimizer(), replicas_to_aggregate=3, total_num_replicas=4)
+
+
+def test_adam_beta_powers_follow_tf_float32_variables():
+    from ba3c_amd.optimizer import AdamOptimizer
+    o = AdamOptimizer(1e-3, beta1=0.8, beta2=0.75)
+    hp0 = o._hparams()
+    o._after_apply()
+    o._after_apply()
+    assert hp0["beta1_power"] == float(np.float32(0.8))
+    assert o.beta1_power == np.float32(np.float32(np.float32(0.8) * np.float32(0.8)) * np.float32(0.8))
+    assert o.beta2_power.dtype == np.float32
+
+
+def test_flags_mirror_run_job():
+    from ba3c_amd.flags import build_parser, resolve
+    a = resolve(build_parser().parse_args(
+        "-b 32 --fc_neurons 128 --fc_splits 4 -o adam --beta1 0.8 --beta2 0.75 --epsilon 1e-8 "
+        "--use_sync -g 60 -l 0.001".split()))
+    assert (a.batch_size, a.fc_neurons, a.fc_splits, a.optimizer, a.ngrads) == (32, 128, 4, "adam", 60)
+    assert a.replace_with_conv is True
+    a = resolve(build_parser().parse_args("--use_normal_fc --adam_debug --beta1 0.7".split()))
+    assert a.replace_with_conv is False and a.beta2 == 0.7
+    with pytest.raises(SystemExit):
+        resolve(build_parser().parse_args(["--use_sync"]))
+
+
+def test_product_engine_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from ba3c_amd import Ba3cLibraryError
+    from ba3c_amd.engine import Ba3cEngine
+    with pytest.raises(Ba3cLibraryError):
+        Ba3cEngine(num_actions=4, fc_neurons=128, fc_splits=4, max_batch=4)
