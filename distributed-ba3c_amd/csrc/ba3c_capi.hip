@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/ba3c.h"
+#include "ba3c_conv.h"
 #include "ba3c_problems.h"
 #include "ba3c_small.h"
 
@@ -61,6 +62,7 @@ struct ba3c_handle {
   int idx_piW, idx_pib, idx_vW, idx_vb;
   int per, wstride;
   TensorTable table;
+  bool band = true;   // band-conv kernels for conv1/conv2 fwd+dgrad (BA3C_GENERIC=1: GEMM engine)
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -72,8 +74,17 @@ struct ba3c_handle {
 namespace {
 
 // ---- workspace layout -----------------------------------------------------------------
+// band-conv geometries (ba3c_conv.h): forward conv1/conv2 with pooling, and the input
+// gradients of conv1/conv2 as VALID convs over the 4-padded un-pooled output gradient
+using GConv1F = BandGeom<40, 40, 32, 32, 5, 5, 6, true, 0, 4>;
+using GConv2F = BandGeom<18, 18, 32, 64, 5, 5, 14, true, 0, 4>;
+using GConv1D = BandGeom<44, 44, 32, 32, 5, 5, 4, false, 1, 8, 4, 4, 18, 18, 36, 36>;
+using GConv2D = BandGeom<22, 22, 64, 32, 5, 5, 6, false, 1, 8, 4, 4, 7, 7, 14, 14>;
+constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
+              WT_C2D = WT_C1D + 800 * 32, WT_TOTAL = WT_C2D + 1600 * 32;
+
 struct Workspace {
-  float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *sumsq;
+  float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *sumsq, *wt;
   uint8_t *c0, *c1, *c2;
   unsigned long long* relu;
   size_t bytes;
@@ -133,6 +144,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   w.a3 = (float*)take(Bz * A3 * 4);
   w.h = (float*)take(Bz * F * 4);
   w.relu = (unsigned long long*)take(RELU_SLOTS * 8);
+  w.wt = (float*)take((size_t)WT_TOTAL * 4);
   if (train) {
     w.c0 = (uint8_t*)take(Bz * P0);
     w.c1 = (uint8_t*)take(Bz * P1);
@@ -200,6 +212,32 @@ int launch_reduce(ba3c_handle* h, hipStream_t s, const float* part, int S, const
     if (_r != BA3C_OK) return _r; \
   } while (0)
 
+template <class G>
+int launch_band(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a) {
+  dim3 grid(a.batch * G::NBANDS);
+  {
+    ProbeScope ps(h, s, kid);
+    hipLaunchKernelGGL(conv_band_kernel<G>, grid, dim3(256), 0, s, a);
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+// [N][K] copies of the band-conv weights for this step (forward; + rotated dgrad in training)
+int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, bool train) {
+  const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
+  const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
+  WPrepArgs a{};
+  a.job[0] = WPrepJob{W1, w.wt + WT_C1F, 5, 5, 32, 32, 0, 800 * 32};
+  a.job[1] = WPrepJob{W2, w.wt + WT_C2F, 5, 5, 32, 64, 0, 800 * 64};
+  a.job[2] = WPrepJob{W1, w.wt + WT_C1D, 5, 5, 32, 32, 1, 800 * 32};
+  a.job[3] = WPrepJob{W2, w.wt + WT_C2D, 5, 5, 32, 64, 1, 1600 * 32};
+  a.njobs = train ? 4 : 2;
+  hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
 // ---- forward --------------------------------------------------------------------------
 template <int CH>
 int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
@@ -210,14 +248,30 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3 = prm + h->tensors[h->idx_conv[3]].offset;
   unsigned long long* rc = train ? w.relu : nullptr;
+  if (h->band) CHECK(launch_wprep(h, s, prm, w, train));
   if (train) {
     ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> c0{state, W0, w.p0, w.c0, rc, 1.0f / 255.0f,
                                                  B * 6400, 32, 25 * CH, 0};
     CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
-    ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> c1{w.p0, W1, w.p1, w.c1, rc, 1.0f, B * 1296, 32, 800, 0};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
-    ConvFwd<false, 18, 18, 32, 32, 5, 5, 64, 0> c2{w.p1, W2, w.p2, w.c2, rc, 1.0f, B * 196, 64, 800, 0};
-    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
+    if (h->band) {
+      CHECK(launch_band<GConv1F>(h, s, BA3C_K_CONV1_FWD,
+                                 BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}));
+      CHECK(launch_band<GConv2F>(h, s, BA3C_K_CONV2_FWD,
+                                 BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B}));
+    } else {
+      ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> c1{w.p0, W1, w.p1, w.c1, rc, 1.0f, B * 1296, 32, 800, 0};
+      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
+      ConvFwd<false, 18, 18, 32, 32, 5, 5, 64, 0> c2{w.p1, W2, w.p2, w.c2, rc, 1.0f, B * 196, 64, 800, 0};
+      CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
+    }
+  } else if (h->band) {
+    ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
+                                                 B * 6400, 32, 25 * CH, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+    CHECK(launch_band<GConv1F>(h, s, BA3C_K_CONV1_FWD,
+                               BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}));
+    CHECK(launch_band<GConv2F>(h, s, BA3C_K_CONV2_FWD,
+                               BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B}));
   } else {
     ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
                                                  B * 6400, 32, 25 * CH, 0};
@@ -305,8 +359,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_WGRAD, g, pl.S)));
     CHECK(conv_reduce(pl, 2, 32, 32));
-    ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
+    if (h->band) {
+      CHECK(launch_band<GConv2D>(h, s, BA3C_K_CONV2_DGRAD,
+                                 BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B}));
+    } else {
+      ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
+      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
+    }
   }
   // conv1
   {
@@ -314,8 +373,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_WGRAD, g, pl.S)));
     CHECK(conv_reduce(pl, 1, 32, 32));
-    ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
+    if (h->band) {
+      CHECK(launch_band<GConv1D>(h, s, BA3C_K_CONV1_DGRAD,
+                                 BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B}));
+    } else {
+      ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
+      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
+    }
   }
   // conv0 (no input gradient: the frames are not trainable)
   {
@@ -385,6 +449,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
     return fail(BA3C_ERR_INVALID, "fc_neurons must be a multiple of 4*fc_splits (or 4*ps)");
   ba3c_handle* h = new ba3c_handle();
   h->cfg = c;
+  if (const char* e = getenv("BA3C_GENERIC")) h->band = !(e[0] == '1');
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
   int64_t off = 0;

@@ -18,16 +18,27 @@ GRAD_TOL = 1e-4
 _ENGINES = {}
 
 
-def engine(A=4, C=4, F=128, S=4, legacy=False, ps=1, max_batch=64):
+def engine(A=4, C=4, F=128, S=4, legacy=False, ps=1, max_batch=64, generic=False):
+    """generic=True selects the gathered-tile GEMM engine for every conv (BA3C_GENERIC=1)
+    instead of the LDS band kernels, so both code paths are held to the oracle."""
+    import os
     from ba3c_amd.engine import Ba3cEngine
-    key = (A, C, F, S, legacy, ps, max_batch)
+    key = (A, C, F, S, legacy, ps, max_batch, generic)
     if key not in _ENGINES:
-        _ENGINES[key] = Ba3cEngine(num_actions=A, channels=C, fc_neurons=F, fc_splits=S,
-                                   replace_with_conv=not legacy, ps=ps, max_batch=max_batch)
+        old = os.environ.get("BA3C_GENERIC")
+        os.environ["BA3C_GENERIC"] = "1" if generic else "0"
+        try:
+            _ENGINES[key] = Ba3cEngine(num_actions=A, channels=C, fc_neurons=F, fc_splits=S,
+                                       replace_with_conv=not legacy, ps=ps, max_batch=max_batch)
+        finally:
+            if old is None:
+                del os.environ["BA3C_GENERIC"]
+            else:
+                os.environ["BA3C_GENERIC"] = old
     return _ENGINES[key]
 
 
-def case(seed, B, A=4, C=4, F=128, S=4, legacy=False, ps=1, wscale=1.0):
+def case(seed, B, A=4, C=4, F=128, S=4, legacy=False, ps=1, wscale=1.0, generic=False):
     rs = np.random.RandomState(seed)
     params = O.init_params(F, S, A, seed=seed, replace_with_conv=not legacy, ps=ps,
                            dtype=np.float32)
@@ -75,6 +86,7 @@ CONFIGS = [
     dict(A=4, C=4, F=128, S=4),                 # BASELINE cfg2 geometry
     dict(A=6, C=12, F=512, S=1),                # RGB x4 frames, default F
     dict(A=18, C=4, F=256, S=1, legacy=True, ps=4),   # --use_normal_fc legacy FC
+    dict(A=4, C=4, F=512, S=1, generic=True),   # gathered-tile GEMM engine for every conv
 ]
 
 
