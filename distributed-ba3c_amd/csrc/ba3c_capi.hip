@@ -18,6 +18,7 @@
 #include "ba3c_conv.h"
 #include "ba3c_problems.h"
 #include "ba3c_small.h"
+#include "ba3c_wgrad.h"
 
 using namespace ba3c;
 
@@ -80,6 +81,11 @@ using GConv1F = BandGeom<40, 40, 32, 32, 5, 5, 6, true, 0, 4>;
 using GConv2F = BandGeom<18, 18, 32, 64, 5, 5, 14, true, 0, 4>;
 using GConv1D = BandGeom<44, 44, 32, 32, 5, 5, 4, false, 1, 8, 4, 4, 18, 18, 36, 36>;
 using GConv2D = BandGeom<22, 22, 64, 32, 5, 5, 6, false, 1, 8, 4, 4, 7, 7, 14, 14>;
+// weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
+using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
+using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
+using GWg2 = WgGeom<18, 18, 32, 5, 5, 64, 7, false, 2>;
+constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
               WT_C2D = WT_C1D + 800 * 32, WT_TOTAL = WT_C2D + 1600 * 32;
 
@@ -123,6 +129,9 @@ size_t max_partials(const ba3c_handle* h, int B) {
   upd(plan_wgrad(576, 64, B * 25, 128, 64));
   upd(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
   upd(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
+  mx = std::max(mx, (size_t)WG_P0 * GWg0::M * 32);
+  mx = std::max(mx, (size_t)WG_P1 * GWg1::M * 32);
+  mx = std::max(mx, (size_t)WG_P2 * GWg2::M * 64);
   return mx;
 }
 
@@ -221,6 +230,27 @@ int launch_band(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a) {
   }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
+}
+
+// persistent weight-gradient band kernel + deterministic reduction into the flat HWIO grads
+template <class G>
+int launch_wgband(ba3c_handle* h, hipStream_t s, int kid, const WgArgs& a, int pmax, float* dst,
+                  int cinpad) {
+  const int nbands = a.batch * G::NBANDS;
+  const int P = std::min(pmax, nbands);
+  {
+    ProbeScope ps(h, s, kid);
+    hipLaunchKernelGGL(wgrad_band_kernel<G>, dim3(P, G::NSPLIT), dim3(256), 0, s, a);
+  }
+  HIP_TRY(hipGetLastError());
+  ReduceMap mp{};
+  mp.kind = 0;
+  mp.M = G::M;
+  mp.N = G::COUT;
+  mp.cin = G::CIN;
+  mp.cinpad = cinpad;
+  mp.dst = dst;
+  return launch_reduce(h, s, a.part, P, mp);
 }
 
 // [N][K] copies of the band-conv weights for this step (forward; + rotated dgrad in training)
@@ -355,10 +385,15 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   }
   // conv2
   {
-    WgradPlan pl = plan_wgrad(800, 64, B * 196, 128, 64);
-    ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_WGRAD, g, pl.S)));
-    CHECK(conv_reduce(pl, 2, 32, 32));
+    if (h->band) {
+      CHECK(launch_wgband<GWg2>(h, s, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part, B}, WG_P2,
+                                grads + h->tensors[h->idx_conv[2]].offset, 32));
+    } else {
+      WgradPlan pl = plan_wgrad(800, 64, B * 196, 128, 64);
+      ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+      CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_WGRAD, g, pl.S)));
+      CHECK(conv_reduce(pl, 2, 32, 32));
+    }
     if (h->band) {
       CHECK(launch_band<GConv2D>(h, s, BA3C_K_CONV2_DGRAD,
                                  BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B}));
@@ -369,10 +404,15 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   }
   // conv1
   {
-    WgradPlan pl = plan_wgrad(800, 32, B * 1296, 128, 32);
-    ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_WGRAD, g, pl.S)));
-    CHECK(conv_reduce(pl, 1, 32, 32));
+    if (h->band) {
+      CHECK(launch_wgband<GWg1>(h, s, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part, B}, WG_P1,
+                                grads + h->tensors[h->idx_conv[1]].offset, 32));
+    } else {
+      WgradPlan pl = plan_wgrad(800, 32, B * 1296, 128, 32);
+      ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_WGRAD, g, pl.S)));
+      CHECK(conv_reduce(pl, 1, 32, 32));
+    }
     if (h->band) {
       CHECK(launch_band<GConv1D>(h, s, BA3C_K_CONV1_DGRAD,
                                  BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B}));
@@ -382,7 +422,10 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
   }
   // conv0 (no input gradient: the frames are not trainable)
-  {
+  if (h->band && CH == 4) {
+    CHECK(launch_wgband<GWg0>(h, s, BA3C_K_CONV0_WGRAD, WgArgs{state, w.dp0, w.c0, w.part, B}, WG_P0,
+                              grads + h->tensors[h->idx_conv[0]].offset, 16));
+  } else {
     WgradPlan pl = plan_wgrad(25 * CH, 32, B * 6400, 128, 32);
     ConvWgrad<true, 84, 84, CH, 5, 5, 32, true> g{state, w.dp0, w.c0, w.part, 1.0f / 255.0f, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_WGRAD, g, pl.S)));
