@@ -87,7 +87,8 @@ using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
 using GWg2 = WgGeom<18, 18, 32, 5, 5, 64, 7, false, 2>;
 constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
-              WT_C2D = WT_C1D + 800 * 32, WT_TOTAL = WT_C2D + 1600 * 32;
+              WT_C2D = WT_C1D + 800 * 32, WT_C0F = WT_C2D + 1600 * 32,
+              WT_TOTAL = WT_C0F + 32 * Conv0Geom::KDIM;
 
 struct Workspace {
   float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *sumsq, *wt;
@@ -265,6 +266,20 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
   a.njobs = train ? 4 : 2;
   hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
+  if (h->cfg.channels == 4) {
+    hipLaunchKernelGGL(conv0_wprep_kernel, dim3((32 * Conv0Geom::KDIM + 255) / 256), dim3(256), 0, s,
+                       prm + h->tensors[h->idx_conv[0]].offset, w.wt + WT_C0F);
+    HIP_TRY(hipGetLastError());
+  }
+  return BA3C_OK;
+}
+
+int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a) {
+  {
+    ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
+    hipLaunchKernelGGL(conv0_band_kernel, dim3(a.batch * Conv0Geom::NBANDS), dim3(256), 0, s, a);
+  }
+  HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
 
@@ -280,9 +295,14 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   unsigned long long* rc = train ? w.relu : nullptr;
   if (h->band) CHECK(launch_wprep(h, s, prm, w, train));
   if (train) {
-    ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> c0{state, W0, w.p0, w.c0, rc, 1.0f / 255.0f,
-                                                 B * 6400, 32, 25 * CH, 0};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+    if (h->band && CH == 4) {
+      CHECK(launch_conv0_band(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
+                                             w.wt + WT_C0F, w.p0, w.c0, rc, B}));
+    } else {
+      ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> c0{state, W0, w.p0, w.c0, rc, 1.0f / 255.0f,
+                                                   B * 6400, 32, 25 * CH, 0};
+      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+    }
     if (h->band) {
       CHECK(launch_band<GConv1F>(h, s, BA3C_K_CONV1_FWD,
                                  BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}));
@@ -295,9 +315,14 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
       CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
     }
   } else if (h->band) {
-    ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
-                                                 B * 6400, 32, 25 * CH, 0};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+    if (CH == 4) {
+      CHECK(launch_conv0_band(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
+                                             w.wt + WT_C0F, w.p0, nullptr, nullptr, B}));
+    } else {
+      ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
+                                                   B * 6400, 32, 25 * CH, 0};
+      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+    }
     CHECK(launch_band<GConv1F>(h, s, BA3C_K_CONV1_FWD,
                                BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}));
     CHECK(launch_band<GConv2F>(h, s, BA3C_K_CONV2_FWD,

@@ -225,6 +225,126 @@ __global__ void __launch_bounds__(256) conv_band_kernel(const BandArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// conv0 forward (train.py:167-185): uint8 frames [B,84,84,4] -> ReLU -> 2x2 max-pool.
+// The band (RB0 + 4 input rows) is staged as x = u8 / 255.0f (exactly train.py:167), one
+// float4 (the 4 frame channels) per pixel.  K = 25 taps x 4 channels is consumed in 7 groups
+// of 4 taps (taps 25..27 have zero weights); in group g, MFMA step t and lane group q cover
+// tap 4g + q, channel t, so one ds_read_b128 of a pixel feeds a lane's 4 steps.  All 112 K
+// values of the wave's 16 output channels stay in 28 registers for the whole band.
+// ---------------------------------------------------------------------------------------
+struct Conv0Geom {
+  static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
+  static constexpr int HO = 80, WO = 80, RB = 8, NBANDS = HO / RB, SROWS = RB + KT - 1;
+  static constexpr int NTG = 7;                             // tap groups of 4
+  static constexpr int KDIM = NTG * 16;                     // 112 (zero-padded K)
+  static constexpr int MROWS = (RB / 2) * (WO / 2) * 4;     // 640 rows = 160 windows
+  static constexpr int MB = MROWS / 16;                     // 40 m-blocks
+  static constexpr int MBW = MB / 2;                        // 20 per wave (2 waves per n-block)
+  static constexpr int MCH = 10;                            // m-blocks per register chunk
+};
+
+__global__ void __launch_bounds__(256) conv0_band_kernel(const BandArgs a) {
+  using G = Conv0Geom;
+  __shared__ float4 xs4[G::SROWS * G::WS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.x / G::NBANDS;
+  const int y0 = (blockIdx.x - img * G::NBANDS) * G::RB;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(a.src);
+  {
+    constexpr int NV = G::SROWS * G::WS;                    // 1008 pixels
+    constexpr int NPT = (NV + 255) / 256;
+    uint32_t v[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int f = tid + 256 * i;
+      v[i] = f < NV ? *reinterpret_cast<const uint32_t*>(src + ((size_t)img * G::HS * G::WS + (size_t)y0 * G::WS + f) * G::C) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int f = tid + 256 * i;
+      if (f < NV)
+        xs4[f] = make_float4((float)(v[i] & 255u) / 255.0f, (float)((v[i] >> 8) & 255u) / 255.0f,
+                             (float)((v[i] >> 16) & 255u) / 255.0f, (float)(v[i] >> 24) / 255.0f);
+    }
+  }
+  const int nb = wave & 1, mb0 = wave >> 1;
+  const int li = lane & 15, lq = lane >> 4;
+  // weights of output channel nb*16+li for this lane's taps 4g+lq, channels 0..3
+  float4 b[G::NTG];
+  const float* wrow = a.wt + (size_t)(nb * 16 + li) * G::KDIM + lq * 4;
+#pragma unroll
+  for (int g = 0; g < G::NTG; ++g) b[g] = *reinterpret_cast<const float4*>(wrow + g * 16);
+  int toff[G::NTG];                                         // this lane's tap offset per group
+#pragma unroll
+  for (int g = 0; g < G::NTG; ++g) {
+    const int tap = 4 * g + lq;
+    toff[g] = tap < G::NTAP ? (tap / G::KT) * G::WS + tap % G::KT : 0;
+  }
+  __syncthreads();
+
+  unsigned long long pos = 0;
+#pragma unroll
+  for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
+    int pbase[G::MCH];
+#pragma unroll
+    for (int j = 0; j < G::MCH; ++j) {
+      const int mb = mb0 + 2 * (ch * G::MCH + j);
+      const int row = mb * 16 + li;
+      const int w = row >> 2, sub = row & 3;
+      const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
+      pbase[j] = (2 * ph + (sub >> 1)) * G::WS + 2 * pw + (sub & 1);
+    }
+    f32x4 acc[G::MCH];
+#pragma unroll
+    for (int j = 0; j < G::MCH; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < G::NTG; ++g) {
+      float4 av[G::MCH];
+#pragma unroll
+      for (int j = 0; j < G::MCH; ++j) av[j] = xs4[pbase[j] + toff[g]];
+#pragma unroll
+      for (int j = 0; j < G::MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].x, b[g].x, acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < G::MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].y, b[g].y, acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < G::MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].z, b[g].z, acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < G::MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j].w, b[g].w, acc[j], 0, 0, 0);
+    }
+    // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nb*16 + li
+    const int col = nb * 16 + li;
+#pragma unroll
+    for (int j = 0; j < G::MCH; ++j) {
+      const int mb = mb0 + 2 * (ch * G::MCH + j);
+      const int w = mb * 4 + lq;
+      const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
+      const float v0 = acc[j][0], v1 = acc[j][1], v2 = acc[j][2], v3 = acc[j][3];
+      pos += (v0 > 0.f) + (v1 > 0.f) + (v2 > 0.f) + (v3 > 0.f);
+      float mx = v0;
+      uint32_t arg = 0;
+      if (v1 > mx) { mx = v1; arg = 1; }
+      if (v2 > mx) { mx = v2; arg = 2; }
+      if (v3 > mx) { mx = v3; arg = 3; }
+      const size_t o = ((size_t)(img * (G::HO / 2) + y0 / 2 + ph) * (G::WO / 2) + pw) * G::COUT + col;
+      a.out[o] = fmaxf(mx, 0.f);
+      if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+    }
+  }
+  if (a.relu_count) relu_count_add(a.relu_count, pos, lane);
+}
+
+// conv0 weights as [32][112]: k = (tap, c) for taps < 25 of the real channels, zero beyond
+__global__ void __launch_bounds__(256) conv0_wprep_kernel(const float* __restrict__ w,
+                                                          float* __restrict__ wt) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 32 * Conv0Geom::KDIM) return;
+  const int o = e / Conv0Geom::KDIM, k = e - o * Conv0Geom::KDIM;
+  const int tap = k >> 2, c = k & 3;
+  // conv0/W is [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99); real channels c < 4
+  wt[e] = tap < Conv0Geom::NTAP ? w[((size_t)tap * 16 + c) * 32 + o] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------
 // Per-step weight preparation: B operand of a band conv as [N][K] with K = (kh, kw, c).
 //   forward:  wt[o][(kh,kw,c)]  = W[kh, kw, c, o]                         (W: [KH,KW,CI,CO])
 //   dgrad:    wt[ci][(a,b,o)]   = W[KH-1-a, KW-1-b, ci, o]
