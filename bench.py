@@ -94,6 +94,71 @@ def time_steps(tr, batch, steps, warmup, world, probe=None):
     return float(el.item())
 
 
+def time_graph_steps(tr, batch, steps, warmup):
+    """Single-GPU small-batch step replayed as one captured hipGraph per step."""
+    replay = tr.capture_step(*batch)
+    for _ in range(warmup):
+        replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        replay()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def overlap_bench(tr, batch, pred_batch, iters, world):
+    """configs[4]: predictor forward of `pred_batch` simulator states on a second HIP stream
+    beside the train step.  The predictor engine reads a parameter snapshot taken at the start
+    of each iteration (stricter than the reference's Hogwild reads)."""
+    from ba3c_amd.engine import Ba3cEngine
+    eng = tr.engine
+    pe = Ba3cEngine(num_actions=eng.num_actions, channels=eng.channels,
+                    fc_neurons=eng.cfg["fc_neurons"], fc_splits=eng.cfg["fc_splits"],
+                    max_batch=pred_batch)
+    g = torch.Generator(device="cuda").manual_seed(4242)
+    states = torch.randint(0, 256, (pred_batch, 84, 84, eng.channels), dtype=torch.uint8,
+                           device="cuda", generator=g)
+    ps = torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+
+    def pred_only():
+        pe.params.copy_(eng.params)
+        pe.forward(states)
+
+    def run(mode, n):
+        sync_all(world)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            if mode in ("train", "both"):
+                if mode == "both":
+                    pe.params.copy_(eng.params)          # snapshot on the learner stream
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                tr.train_step(*batch)
+            if mode == "pred":
+                pred_only()
+            if mode == "both":
+                ps.wait_event(ev)
+                with torch.cuda.stream(ps):
+                    pe.forward(states)
+                main.wait_stream(ps)
+        sync_all(world)
+        return (time.perf_counter() - t0) / n * 1000.0
+
+    run("both", 2)
+    t_train = run("train", iters)
+    t_pred = run("pred", iters)
+    t_both = run("both", iters)
+    B = batch[0].shape[0]
+    return {"config": "configs[4]: predictor forward of %d states/GPU + train step (B=%d) on "
+                      "separate HIP streams" % (pred_batch, B),
+            "train_ms": round(t_train, 4), "predict_ms": round(t_pred, 4),
+            "overlapped_ms": round(t_both, 4),
+            "overlap_speedup": round((t_train + t_pred) / t_both, 3),
+            "predict_states_per_s": round(world * pred_batch / (t_pred / 1000.0), 1)}
+
+
 def find_dominant_kernel(tr, batch):
     from ba3c_amd._lib import KERNEL_IDS
     eng = tr.engine
@@ -157,6 +222,8 @@ def main():
     ap.add_argument("--num_actions", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-b32", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--predict_batch", type=int, default=8192)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -212,14 +279,20 @@ def main():
            "roofline": roof,
            "kernel_ms_one_step": {k: round(v, 4) for k, v in per_kernel.items()}}
 
+    if not args.no_overlap:
+        out["overlap"] = overlap_bench(tr, batch, args.predict_batch, 10, world)
     if not args.no_b32:
         del tr
         tr32, b32 = build_trainer(32, 128, 4, A, world, seed=rank)
-        el32 = time_steps(tr32, b32, max(args.steps, 50), 10, world)
-        n32 = max(args.steps, 50)
+        n32 = max(args.steps, 100)
+        el32 = time_steps(tr32, b32, n32, 10, world)
         out["b32"] = {"config": "configs[1]: B=32/GPU, fc_neurons=128, fc_splits=4",
                       "value": round(world * 32 * n32 / el32, 1), "unit": "samples/s",
-                      "ms_per_step": round(el32 / n32 * 1000.0, 4)}
+                      "ms_per_step": round(el32 / n32 * 1000.0, 4), "launch": "eager"}
+        if world == 1:
+            elg = time_graph_steps(tr32, b32, n32, 10)
+            out["b32"].update({"value_graph": round(32 * n32 / elg, 1),
+                               "ms_per_step_graph": round(elg / n32 * 1000.0, 4)})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(F, S, A, args.cpu_seconds)
     if rank == 0:

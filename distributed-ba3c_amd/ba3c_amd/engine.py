@@ -158,14 +158,24 @@ class Ba3cEngine(object):
         _lib.check(self.lib.ba3c_clip_grads(self.h, _stream(), _ptr(grads),
                                             _ptr(self._workspace(True))))
 
-    def apply_update(self, opt, slot0, slot1, hp, grad_scale=1.0, fuse_clip=False, grads=None):
+    def apply_update(self, opt, slot0, slot1, hp, grad_scale=1.0, fuse_clip=False, grads=None,
+                     dev_powers=None):
+        """One optimizer apply; dev_powers (float32 device tensor [2]) keeps Adam's
+        beta-power state on the GPU (required inside a captured hipGraph)."""
         grads = self.grads if grads is None else grads
         p = _lib.Ba3cOptParams(**hp)
-        _lib.check(self.lib.ba3c_apply_update(self.h, _stream(), _lib.OPT_IDS[opt],
-                                              _ptr(self.params), _ptr(grads), _ptr(slot0),
-                                              _ptr(slot1), ctypes.byref(p), float(grad_scale),
-                                              1 if fuse_clip else 0,
-                                              _ptr(self._workspace(True))))
+        if dev_powers is None:
+            _lib.check(self.lib.ba3c_apply_update(self.h, _stream(), _lib.OPT_IDS[opt],
+                                                  _ptr(self.params), _ptr(grads), _ptr(slot0),
+                                                  _ptr(slot1), ctypes.byref(p), float(grad_scale),
+                                                  1 if fuse_clip else 0,
+                                                  _ptr(self._workspace(True))))
+        else:
+            _lib.check(self.lib.ba3c_apply_update_dev(self.h, _stream(), _lib.OPT_IDS[opt],
+                                                      _ptr(self.params), _ptr(grads), _ptr(slot0),
+                                                      _ptr(slot1), ctypes.byref(p), _ptr(dev_powers),
+                                                      float(grad_scale), 1 if fuse_clip else 0,
+                                                      _ptr(self._workspace(True))))
 
     def sample(self, probs, u, actions=None, flag=None):
         """numpy RandomState.choice(A, p) given the uniform draws u (float64 device tensor)."""

@@ -31,6 +31,8 @@ class Optimizer(object):
     def _after_apply(self):
         pass
 
+    dev_powers = None
+
     def apply_gradients(self, engine, grad_scale=1.0, fuse_clip=False, grads=None):
         """optimizer.apply_gradients(grads) (train/multigpu.py:194) over engine.grads."""
         if self.slots is None:
@@ -38,7 +40,7 @@ class Optimizer(object):
         s0 = self.slots[0] if len(self.slots) > 0 else None
         s1 = self.slots[1] if len(self.slots) > 1 else None
         engine.apply_update(self.opt_id, s0, s1, self._hparams(), grad_scale=grad_scale,
-                            fuse_clip=fuse_clip, grads=grads)
+                            fuse_clip=fuse_clip, grads=grads, dev_powers=self.dev_powers)
         self._after_apply()
 
     def slot_dict(self, engine, i):
@@ -66,8 +68,23 @@ class AdamOptimizer(Optimizer):
         return h
 
     def _after_apply(self):
+        if self.dev_powers is not None:
+            return                       # the GPU multiplies its own copy (graph-safe)
         self.beta1_power = _f(self.beta1_power * _f(self.beta1))
         self.beta2_power = _f(self.beta2_power * _f(self.beta2))
+
+    def use_device_state(self, device):
+        """Move beta1_power/beta2_power to a device tensor updated by the update kernel's
+        stream, so the whole step can be captured once and replayed as a hipGraph."""
+        if self.dev_powers is None:
+            self.dev_powers = torch.tensor([self.beta1_power, self.beta2_power],
+                                           dtype=torch.float32, device=device)
+
+    def powers(self):
+        if self.dev_powers is not None:
+            v = self.dev_powers.cpu().numpy()
+            return _f(v[0]), _f(v[1])
+        return self.beta1_power, self.beta2_power
 
 
 class RMSPropOptimizer(Optimizer):

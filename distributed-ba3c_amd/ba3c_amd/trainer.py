@@ -66,6 +66,31 @@ class Ba3cTrainer(object):
             opt.apply_gradients(self.engine)
         self.global_step += 1
 
+    def capture_step(self, state, action, futurereward, warmup=2):
+        """Capture one full step (fwd+bwd+clip+update) on static input tensors as a hipGraph
+        (torch.cuda.CUDAGraph over the HIP stream).  Returns a callable that replays it; the
+        caller refills `state`/`action`/`futurereward` in place between replays.  Adam's
+        beta powers move to the device so every replay uses the right bias correction."""
+        opt = self.optimizer
+        inner = opt._opt if isinstance(opt, SyncReplicasOptimizer) else opt
+        if hasattr(inner, "use_device_state"):
+            inner.use_device_state(self.engine.device)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.train_step(state, action, futurereward)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self.train_step(state, action, futurereward)
+        self.global_step -= 1                 # capture records the step, it does not run it
+
+        def replay():
+            graph.replay()
+            self.global_step += 1
+        return replay
+
     def run_step(self, batch):
         """batch = [state, action, futurereward, ts, init_R, isOver] (train.py:432) as numpy or
         tensors; returns the TfDictOp dict incl. global_step and dp_per_s (multigpu.py:307-313)."""

@@ -688,9 +688,10 @@ int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace)
   return BA3C_OK;
 }
 
-int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
-                      const float* grads, float* slot0, float* slot1, const ba3c_opt_params* hp,
-                      float grad_scale, int32_t fuse_clip, void* workspace) {
+static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* params,
+                             const float* grads, float* slot0, float* slot1,
+                             const ba3c_opt_params* hp, float* dev_powers, float grad_scale,
+                             int32_t fuse_clip, void* workspace) {
   if (!h || !hp || !check_ptr(params) || !check_ptr(grads)) return fail(BA3C_ERR_INVALID, "null pointer");
   const bool need0 = opt != BA3C_OPT_GD, need1 = opt == BA3C_OPT_ADAM || opt == BA3C_OPT_RMS || opt == BA3C_OPT_ADADELTA;
   if ((need0 && !check_ptr(slot0)) || (need1 && !check_ptr(slot1)))
@@ -705,7 +706,8 @@ int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
   a.grad_scale = grad_scale;
   a.lr = hp->lr;
   // TF-1.2 float32 scalar arithmetic of ApplyAdam: alpha = lr*sqrt(1-b2^t)/(1-b1^t)
-  a.alpha = (hp->lr * sqrtf(1.0f - hp->beta2_power)) / (1.0f - hp->beta1_power);
+  a.alpha = dev_powers ? 0.f : adam_alpha(hp->lr, hp->beta1_power, hp->beta2_power);
+  a.dev_powers = dev_powers;
   a.one_minus_b1 = 1.0f - hp->beta1;
   a.one_minus_b2 = 1.0f - hp->beta2;
   a.eps = hp->epsilon;
@@ -733,7 +735,28 @@ int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
     }
   }
   HIP_TRY(hipGetLastError());
+  if (opt == BA3C_OPT_ADAM && dev_powers) {
+    hipLaunchKernelGGL(adam_powers_kernel, dim3(1), dim3(64), 0, s, dev_powers, hp->beta1, hp->beta2);
+    HIP_TRY(hipGetLastError());
+  }
   return BA3C_OK;
+}
+
+int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
+                      const float* grads, float* slot0, float* slot1, const ba3c_opt_params* hp,
+                      float grad_scale, int32_t fuse_clip, void* workspace) {
+  return apply_update_impl(h, stream, opt, params, grads, slot0, slot1, hp, nullptr, grad_scale,
+                           fuse_clip, workspace);
+}
+
+int ba3c_apply_update_dev(ba3c_handle* h, void* stream, int32_t opt, float* params,
+                          const float* grads, float* slot0, float* slot1,
+                          const ba3c_opt_params* hp, float* dev_powers, float grad_scale,
+                          int32_t fuse_clip, void* workspace) {
+  if (opt == BA3C_OPT_ADAM && !check_ptr(dev_powers) && dev_powers == nullptr)
+    return fail(BA3C_ERR_INVALID, "dev_powers required");
+  return apply_update_impl(h, stream, opt, params, grads, slot0, slot1, hp, dev_powers, grad_scale,
+                           fuse_clip, workspace);
 }
 
 int ba3c_sample(void* stream, const float* probs, const double* u, int32_t batch,

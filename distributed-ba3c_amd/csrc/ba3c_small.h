@@ -352,7 +352,21 @@ struct UpdateArgs {
   float grad_scale;
   float lr, one_minus_b1, one_minus_b2, eps, alpha;   // adam
   float decay_c, momentum, rho, one_minus_rho;        // rms (decay_c = 1-decay), momentum, adadelta
+  const float* dev_powers;  // non-null: Adam beta1^t, beta2^t read from the device (graph-safe)
 };
+
+// TF-1.2 float32 scalar arithmetic of ApplyAdam: alpha = lr*sqrt(1-b2^t)/(1-b1^t)
+__host__ __device__ __forceinline__ float adam_alpha(float lr, float b1p, float b2p) {
+  return (lr * sqrtf(1.0f - b2p)) / (1.0f - b1p);
+}
+
+// beta*_power.assign(beta*_power * beta*) after the apply (train.py:584 optimizer state)
+__global__ void adam_powers_kernel(float* powers, float beta1, float beta2) {
+  if (threadIdx.x == 0) {
+    powers[0] = powers[0] * beta1;
+    powers[1] = powers[1] * beta2;
+  }
+}
 
 template <int OPT>
 __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const TensorTable tt) {
@@ -363,6 +377,8 @@ __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const T
   const int end = min(tt.numel[t], beg + UPD_CHUNK);
   const long long o = tt.off[t];
   const float f = a.clip_part ? clip_factor(tt, t, a.clip_part) : 0.f;
+  const float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1])
+                                                 : a.alpha;
   for (int i = beg + threadIdx.x; i < end; i += 256) {
     const long long k = o + i;
     float g = a.g[k];
@@ -372,7 +388,7 @@ __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const T
       float m = a.s0[k], v = a.s1[k];
       m += (g - m) * a.one_minus_b1;
       v += (g * g - v) * a.one_minus_b2;
-      p -= (m * a.alpha) / (sqrtf(v) + a.eps);
+      p -= (m * alpha) / (sqrtf(v) + a.eps);
       a.s0[k] = m;
       a.s1[k] = v;
     } else if constexpr (OPT == 1) {  // ApplyGradientDescent

@@ -151,6 +151,15 @@ int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
                       const ba3c_opt_params* hp, float grad_scale, int32_t fuse_clip,
                       void* workspace);
 
+/* Same apply with the Adam bias-correction state on the device: dev_powers = {beta1_power,
+ * beta2_power} (float32, TF's variables) is read by the update and multiplied by
+ * (beta1, beta2) after it, on the stream — so a captured hipGraph of the whole step replays
+ * with the correct per-step alpha.  hp->beta*_power are ignored. */
+int ba3c_apply_update_dev(ba3c_handle* h, void* stream, int32_t opt, float* params,
+                          const float* grads, float* slot0, float* slot1,
+                          const ba3c_opt_params* hp, float* dev_powers, float grad_scale,
+                          int32_t fuse_clip, void* workspace);
+
 /* Action sampling: actions[i] = #{k : cdf_i[k] <= u[i]} with cdf_i = cumsum(double(p_i))
  * / cdf_i[A-1]  (numpy RandomState.choice).  nonfinite (device int32, may be NULL) is
  * set to 1 if any probability is not finite (train.py:381 assert). */

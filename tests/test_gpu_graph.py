@@ -1,0 +1,55 @@
+"""hipGraph-captured learner step (Ba3cTrainer.capture_step): replaying the captured
+fwd+bwd+clip+Adam chain, with the inputs refilled in place between replays, reproduces the
+eager step sequence bit for bit — Adam's bias-correction powers live on the device, so every
+replay uses the step count's own alpha (TF's float32 beta-power variables)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ba3c_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(B):
+    from ba3c_amd.model import Model
+    from ba3c_amd.optimizer import AdamOptimizer
+    from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
+    m = Model(num_actions=4, fc_neurons=128, fc_splits=4, batch_size=B, max_batch=B)
+    m.engine.load_params(O.init_params(128, 4, 4, seed=5, dtype=np.float32))
+    return Ba3cTrainer(TrainConfig(model=m, optimizer=AdamOptimizer(1e-3, 0.8, 0.75, 1e-8)))
+
+
+def _batches(B, n):
+    out = []
+    for i in range(n):
+        rs = np.random.RandomState(300 + i)
+        out.append((torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda(),
+                    torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda(),
+                    torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()))
+    return out
+
+
+def test_captured_step_replays_match_eager_steps():
+    B = 16
+    bs = _batches(B, 4)
+    eager = _trainer(B)
+    for b in [bs[0], bs[0]] + bs[1:]:       # capture_step's two warmup steps use the first batch
+        eager.train_step(*b)
+    torch.cuda.synchronize()
+
+    cap = _trainer(B)
+    static = tuple(t.clone() for t in bs[0])
+    replay = cap.capture_step(*static, warmup=2)
+    for b in bs[1:]:
+        for dst, src in zip(static, b):
+            dst.copy_(src)
+        replay()
+    torch.cuda.synchronize()
+    assert cap.global_step == eager.global_step == 5
+    np.testing.assert_array_equal(cap.engine.params.cpu().numpy(), eager.engine.params.cpu().numpy())
+    b1, b2 = cap.optimizer.powers()
+    e1, e2 = eager.optimizer.powers()
+    assert (b1, b2) == (e1, e2)
+    for s_cap, s_eag in zip(cap.optimizer.slots, eager.optimizer.slots):
+        np.testing.assert_array_equal(s_cap.cpu().numpy(), s_eag.cpu().numpy())

@@ -1,0 +1,111 @@
+"""Predictor path on the GPU: the ModelDesc-mirror Model in a 'towerp0' TowerContext,
+OnlinePredictor's list-in/list-out convention (predict/base.py:80-92) and the batched
+MultiThreadAsyncPredictor (predict/concurrency.py:172-219) whose callbacks receive actions
+drawn with numpy's RandomState.choice semantics from the same uniform stream."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ba3c_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(B=64):
+    from ba3c_amd.model import Model
+    m = Model(num_actions=4, channels=1, fc_neurons=128, fc_splits=4, batch_size=B, max_batch=B)
+    p32 = O.init_params(128, 4, 4, seed=3, dtype=np.float32)
+    m.engine.load_params(p32)
+    return m, {k: v.astype(np.float64) for k, v in p32.items()}
+
+
+def test_tower_context_prediction_graph():
+    from ba3c_amd.model_desc import TowerContext
+    m, p64 = _model()
+    state = np.random.RandomState(0).randint(0, 256, size=(6, 84, 84, 4)).astype(np.uint8)
+    m.explore_factor = 2.0
+    with TowerContext("towerp0"):
+        m.build_graph([torch.from_numpy(state).cuda(), None, None])
+    t = O.get_nn_prediction(p64, state, {"fc_neurons": 128, "fc_splits": 4}, explore_factor=2.0)
+    assert np.abs(m.logitsT.cpu().numpy() - t["logitsT"]).max() < 1e-5
+
+
+def test_online_predictor_convention():
+    m, p64 = _model()
+    f = m.get_predict_func(["state"], ["logitsT", "pred_value"])
+    state = np.random.RandomState(1).randint(0, 256, size=(3, 84, 84, 4)).astype(np.uint8)
+    out = f([state])
+    assert len(out) == 4 and out[3] is True
+    t = O.get_nn_prediction(p64, state, {"fc_neurons": 128, "fc_splits": 4})
+    assert np.abs(out[0].cpu().numpy() - t["logitsT"]).max() < 1e-5
+    bad = f([np.zeros((2, 84, 84, 7), np.uint8)])          # wrong channel count
+    assert bad[3] is False and bad[0].shape == (2, 4)
+
+
+def test_async_predictor_batches_and_samples_like_numpy():
+    from ba3c_amd.predict import MultiThreadAsyncPredictor
+    m, p64 = _model(B=64)
+    pred = MultiThreadAsyncPredictor(m.get_predict_func(), batch_size=64,
+                                     rs=np.random.RandomState(77))
+    states = np.random.RandomState(2).randint(0, 256, size=(40, 84, 84, 4)).astype(np.uint8)
+    results = {}
+    done = threading.Event()
+
+    def cb(i):
+        def f(o):
+            results[i] = o
+            if len(results) == len(states):
+                done.set()
+        return f
+
+    for i in range(len(states)):
+        pred.put_task([states[i]], cb(i))
+    pred.run()
+    assert done.wait(60)
+    pred.stop()
+    t = O.get_nn_prediction(p64, states, {"fc_neurons": 128, "fc_splits": 4})
+    probs = np.stack([results[i][0] for i in range(len(states))])
+    assert np.abs(probs - t["logitsT"]).max() < 1e-5
+    # actions: numpy's choice on the GPU probabilities with the same RandomState stream
+    acts = np.array([results[i][4] for i in range(len(states))])
+    ref = O.np_random_choice(probs, np.random.RandomState(77))
+    np.testing.assert_array_equal(acts, ref)
+
+
+def test_large_batch_forward_is_batch_independent():
+    """One 2048-state forward equals forwards of sub-batches bit for bit (every kernel's
+    accumulation order per state is independent of the batch it runs in)."""
+    from ba3c_amd.engine import Ba3cEngine
+    eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=2048)
+    eng.load_params(O.init_params(512, 1, 4, seed=5, dtype=np.float32))
+    g = torch.Generator(device="cuda").manual_seed(0)
+    state = torch.randint(0, 256, (2048, 84, 84, 4), dtype=torch.uint8, device="cuda", generator=g)
+    p_all, _, v_all = [x.clone() for x in eng.forward(state)]
+    for lo, hi in ((0, 1), (5, 37), (1000, 2048)):
+        p, _, v = eng.forward(state[lo:hi].contiguous())
+        assert torch.equal(p, p_all[lo:hi]) and torch.equal(v, v_all[lo:hi])
+
+
+def test_full_size_gradient_is_batch_mean_of_halves():
+    """B=2048/F=512 (the bench workload): the gradient of the batch mean equals the weighted
+    mean of the two half-batch gradients (size-independent linearity check, 1e-5)."""
+    from ba3c_amd.engine import Ba3cEngine
+    eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=2048)
+    eng.load_params(O.init_params(512, 1, 4, seed=6, dtype=np.float32))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    B = 2048
+    state = torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device="cuda", generator=g)
+    action = torch.randint(0, 4, (B,), dtype=torch.int64, device="cuda", generator=g)
+    R = torch.randn(B, dtype=torch.float32, device="cuda", generator=g)
+    eng.train_grads(state, action, R)
+    full = eng.grads.clone()
+    h = B // 2
+    eng.train_grads(state[:h].contiguous(), action[:h].contiguous(), R[:h].contiguous())
+    g1 = eng.grads.clone()
+    eng.train_grads(state[h:].contiguous(), action[h:].contiguous(), R[h:].contiguous())
+    g2 = eng.grads.clone()
+    mix = (g1.double() + g2.double()) / 2
+    err = (full.double() - mix).abs().max() / full.double().abs().max()
+    assert err < 1e-5, float(err)

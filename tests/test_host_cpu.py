@@ -58,7 +58,8 @@ class OracleEngine(object):
         self.grads.copy_(torch.from_numpy(np.concatenate(
             [O.clip_by_average_norm(g[k]).reshape(-1) for k in self.names])))
 
-    def apply_update(self, opt, slot0, slot1, hp, grad_scale=1.0, fuse_clip=False, grads=None):
+    def apply_update(self, opt, slot0, slot1, hp, grad_scale=1.0, fuse_clip=False, grads=None,
+                     dev_powers=None):
         assert opt == "adam"
         if fuse_clip:
             self.clip_grads()
