@@ -18,6 +18,7 @@
 #include "ba3c_conv.h"
 #include "ba3c_problems.h"
 #include "ba3c_small.h"
+#include "ba3c_split.h"
 #include "ba3c_wgrad.h"
 
 using namespace ba3c;
@@ -64,6 +65,7 @@ struct ba3c_handle {
   int per, wstride;
   TensorTable table;
   bool band = true;   // band-conv kernels for conv1/conv2 fwd+dgrad (BA3C_GENERIC=1: GEMM engine)
+  bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -86,9 +88,11 @@ using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
 using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
 using GWg2 = WgGeom<18, 18, 32, 5, 5, 64, 7, false, 2>;
 constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
+constexpr int WG_P0S = 256;   // conv0s_wgrad_kernel: one 141 KB-LDS workgroup per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
               WT_C2D = WT_C1D + 800 * 32, WT_C0F = WT_C2D + 1600 * 32,
-              WT_TOTAL = WT_C0F + 32 * Conv0Geom::KDIM;
+              WT_C0S = WT_C0F + 32 * Conv0Geom::KDIM,            // uint4 [Conv0S::WB_U4]
+              WT_TOTAL = WT_C0S + 4 * Conv0S::WB_U4;
 
 struct Workspace {
   float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *sumsq, *wt;
@@ -131,6 +135,7 @@ size_t max_partials(const ba3c_handle* h, int B) {
   upd(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
   upd(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
   mx = std::max(mx, (size_t)WG_P0 * GWg0::M * 32);
+  mx = std::max(mx, (size_t)4 * WG_P0S * Conv0W::M * 32);
   mx = std::max(mx, (size_t)WG_P1 * GWg1::M * 32);
   mx = std::max(mx, (size_t)WG_P2 * GWg2::M * 64);
   return mx;
@@ -266,7 +271,12 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
   a.njobs = train ? 4 : 2;
   hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
-  if (h->cfg.channels == 4) {
+  if (h->cfg.channels == 4 && h->split) {
+    hipLaunchKernelGGL(conv0s_wprep_kernel, dim3((2 * Conv0S::KSTEPS * 64 + 255) / 256), dim3(256), 0,
+                       s, prm + h->tensors[h->idx_conv[0]].offset,
+                       reinterpret_cast<uint4*>(w.wt + WT_C0S));
+    HIP_TRY(hipGetLastError());
+  } else if (h->cfg.channels == 4) {
     hipLaunchKernelGGL(conv0_wprep_kernel, dim3((32 * Conv0Geom::KDIM + 255) / 256), dim3(256), 0, s,
                        prm + h->tensors[h->idx_conv[0]].offset, w.wt + WT_C0F);
     HIP_TRY(hipGetLastError());
@@ -275,7 +285,13 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
 }
 
 int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a) {
-  {
+  if (h->split) {
+    const Conv0SArgs sa{reinterpret_cast<const uint8_t*>(a.src),
+                        reinterpret_cast<const uint4*>(a.wt - WT_C0F + WT_C0S), a.out, a.out_code,
+                        a.relu_count, a.batch};
+    ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
+    hipLaunchKernelGGL(conv0s_fwd_kernel, dim3(a.batch * Conv0S::NBANDS), dim3(256), 0, s, sa);
+  } else {
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
     hipLaunchKernelGGL(conv0_band_kernel, dim3(a.batch * Conv0Geom::NBANDS), dim3(256), 0, s, a);
   }
@@ -447,7 +463,23 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
   }
   // conv0 (no input gradient: the frames are not trainable)
-  if (h->band && CH == 4) {
+  if (h->band && CH == 4 && h->split) {
+    const int P = std::min(WG_P0S, B * Conv0W::NBANDS);
+    {
+      ProbeScope ps(h, s, BA3C_K_CONV0_WGRAD);
+      hipLaunchKernelGGL(conv0s_wgrad_kernel, dim3(P), dim3(256), 0, s,
+                         Conv0WArgs{state, w.dp0, w.c0, w.part, B});
+    }
+    HIP_TRY(hipGetLastError());
+    ReduceMap mp{};
+    mp.kind = 0;
+    mp.M = Conv0W::M;
+    mp.N = 32;
+    mp.cin = 4;
+    mp.cinpad = 16;
+    mp.dst = grads + h->tensors[h->idx_conv[0]].offset;
+    CHECK(launch_reduce(h, s, w.part, 4 * P, mp));
+  } else if (h->band && CH == 4) {
     CHECK(launch_wgband<GWg0>(h, s, BA3C_K_CONV0_WGRAD, WgArgs{state, w.dp0, w.c0, w.part, B}, WG_P0,
                               grads + h->tensors[h->idx_conv[0]].offset, 16));
   } else {
@@ -518,6 +550,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   ba3c_handle* h = new ba3c_handle();
   h->cfg = c;
   if (const char* e = getenv("BA3C_GENERIC")) h->band = !(e[0] == '1');
+  if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
   int64_t off = 0;

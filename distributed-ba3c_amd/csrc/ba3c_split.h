@@ -1,0 +1,396 @@
+// ba3c_split.h — conv0 on bf16 MFMA with exact operand splitting (gfx950).
+//
+// conv0 (train.py:167-185) multiplies uint8 frame values by fp32 weights.  Every value 0..255
+// is exact in bf16 (8 significant bits), and every fp32 weight w is exactly the sum of three
+// bf16 numbers hi + mid + lo (8 + 8 + 8 significant bits, round-to-nearest at each stage,
+// each residual exact in fp32).  So
+//
+//     sum_k u8_k * w_k  =  sum_k u8_k * hi_k + sum_k u8_k * mid_k + sum_k u8_k * lo_k
+//
+// where every product is exact (16 significant bits) and the sums accumulate in fp32 inside
+// v_mfma_f32_16x16x32_bf16: three bf16 MFMAs give the fp32 convolution at fp32 accumulation
+// accuracy, at 16/3 the fp32 MFMA rate.  The result is scaled by 1/255 once (TF scales each
+// frame value first, train.py:167; both are within fp32 rounding of the exact sum).
+//
+// Operand layout of v_mfma_f32_16x16x32_bf16: lane l supplies row/column (l & 15) and eight
+// K values of lane group q = l >> 4.  Only A and B agreeing on the K order matters, so
+// K-step s, lane group q, element e is tap 8s + 2q + (e >> 2), frame channel e & 3: a lane's
+// A fragment is two 8-byte LDS reads (two taps x 4 channels of one bf16 pixel).
+#pragma once
+#include "ba3c_conv.h"
+
+namespace ba3c {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint2 a, uint2 b) {
+  u32x4 u = {a.x, a.y, b.x, b.y};
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// bf16 bits of a small non-negative integer (exact: <= 8 significant bits)
+__device__ __forceinline__ uint32_t u8_bf16(uint32_t v) { return __float_as_uint((float)v) >> 16; }
+
+// round-to-nearest-even fp32 -> bf16 bits (finite inputs) and back
+__device__ __forceinline__ uint32_t f32_bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_f32(uint32_t b) { return __uint_as_float(b << 16); }
+
+// w = hi + mid + lo exactly (bf16 bits)
+__device__ __forceinline__ void split3(float w, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+  hi = f32_bf16_rne(w);
+  const float r1 = w - bf16_f32(hi);
+  mid = f32_bf16_rne(r1);
+  const float r2 = r1 - bf16_f32(mid);
+  lo = f32_bf16_rne(r2);
+}
+
+struct Conv0S {
+  static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
+  static constexpr int HO = 80, WO = 80, RB = 16, NBANDS = HO / RB, SROWS = RB + KT - 1;
+  static constexpr int KSTEPS = 4;                 // 4 x 32 K = 32 tap slots (25 used)
+  static constexpr int NSPLIT = 3;
+  static constexpr int PROWS_W = RB / 2 / 4;       // pooled rows per wave (2)
+  static constexpr int MBROW = (WO / 2) / 4;       // m-blocks per pooled row (10)
+  static constexpr int MBW = PROWS_W * MBROW;      // m-blocks per wave (20)
+  static constexpr int MCH = 5;                    // m-blocks per accumulator chunk
+  // prepared weights: [split][nt][kstep][lane] x 16 bytes
+  static constexpr int WB_U4 = NSPLIT * 2 * KSTEPS * 64;
+  static_assert(RB % 8 == 0 && HO % RB == 0 && MBW % MCH == 0, "conv0 split geometry");
+};
+
+// conv0/W [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99; real channels c < 4) -> bf16 splits
+// in MFMA B-fragment order.  One thread per (nt, kstep, lane).
+__global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restrict__ w,
+                                                           uint4* __restrict__ wb) {
+  using G = Conv0S;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * G::KSTEPS * 64) return;
+  const int lane = t & 63, s = (t >> 6) % G::KSTEPS, nt = t / (64 * G::KSTEPS);
+  const int n = nt * 16 + (lane & 15), q = lane >> 4;
+  uint32_t part[3][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int tap = 8 * s + 2 * q + (e >> 2), c = e & 3;
+    const float v = tap < G::NTAP ? w[((size_t)tap * 16 + c) * 32 + n] : 0.f;
+    split3(v, part[0][e], part[1][e], part[2][e]);
+  }
+#pragma unroll
+  for (int sp = 0; sp < 3; ++sp)
+    wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane] =
+        make_uint4(part[sp][0] | (part[sp][1] << 16), part[sp][2] | (part[sp][3] << 16),
+                   part[sp][4] | (part[sp][5] << 16), part[sp][6] | (part[sp][7] << 16));
+}
+
+// One workgroup = one image x one band of RB output rows (RB/2 pooled rows); wave w owns
+// pooled rows 2w, 2w+1 of the band = 20 m-blocks of 4 windows, both 16-channel n-tiles.
+// M rows are ordered (window, sub) so a lane's 4 accumulator rows are one 2x2 window.
+struct Conv0SArgs {
+  const uint8_t* x;        // frames [B,84,84,4]
+  const uint4* wb;         // prepared bf16 weight splits
+  float* out;              // pooled [B,40,40,32]
+  uint8_t* out_code;       // argmax codes (may be null)
+  unsigned long long* relu_count;
+  int batch;
+};
+
+__global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
+  using G = Conv0S;
+  __shared__ uint2 xs[G::SROWS * G::WS];            // bf16 pixels (4 channels), 13.4 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.x / G::NBANDS;
+  const int y0 = (blockIdx.x - img * G::NBANDS) * G::RB;
+
+  // ---- stage rows [y0, y0 + SROWS): contiguous 16-byte loads (4 pixels), all in flight ----
+  {
+    constexpr int NV = G::SROWS * G::WS / 4;       // 420 uint4
+    constexpr int NPT = (NV + 255) / 256;
+    const uint4* src = reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
+    uint4 v[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int f = tid + 256 * i;
+      v[i] = f < NV ? src[f] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int f = tid + 256 * i;
+      if (f < NV) {
+        const uint32_t px[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        uint4 lo, hi;
+        uint32_t o[8];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          o[2 * p] = u8_bf16(px[p] & 255u) | (u8_bf16((px[p] >> 8) & 255u) << 16);
+          o[2 * p + 1] = u8_bf16((px[p] >> 16) & 255u) | (u8_bf16(px[p] >> 24) << 16);
+        }
+        lo = make_uint4(o[0], o[1], o[2], o[3]);
+        hi = make_uint4(o[4], o[5], o[6], o[7]);
+        reinterpret_cast<uint4*>(xs)[2 * f] = lo;
+        reinterpret_cast<uint4*>(xs)[2 * f + 1] = hi;
+      }
+    }
+  }
+
+  const int li = lane & 15, lq = lane >> 4;
+  bf16x8 wf[G::NSPLIT][2][G::KSTEPS];
+#pragma unroll
+  for (int sp = 0; sp < G::NSPLIT; ++sp)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int s = 0; s < G::KSTEPS; ++s) {
+        const uint4 u = a.wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane];
+        wf[sp][nt][s] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+      }
+  // this lane's row (window li>>2, sub li&3) of m-block 0 of the wave, per (kstep, tap half)
+  const int wi = li >> 2, sub = li & 3;
+  const int pix0 = (4 * wave + (sub >> 1)) * G::WS + 2 * wi + (sub & 1);
+  int lb[G::KSTEPS][2];
+#pragma unroll
+  for (int s = 0; s < G::KSTEPS; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int tap = 8 * s + 2 * lq + h;
+      lb[s][h] = pix0 + (tap < G::NTAP ? (tap / G::KT) * G::WS + tap % G::KT : 0);
+    }
+  __syncthreads();
+
+  unsigned long long pos = 0;
+  const float inv255 = 1.0f / 255.0f;
+#pragma unroll
+  for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
+    f32x4 acc[G::MCH][2];
+#pragma unroll
+    for (int j = 0; j < G::MCH; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < G::KSTEPS; ++s) {
+      bf16x8 af[G::MCH];
+#pragma unroll
+      for (int j = 0; j < G::MCH; ++j) {
+        const int jj = ch * G::MCH + j;
+        const int off = (jj / G::MBROW) * 2 * G::WS + (jj % G::MBROW) * 8;   // immediate
+        af[j] = as_bf16x8(xs[lb[s][0] + off], xs[lb[s][1] + off]);
+      }
+#pragma unroll
+      for (int sp = 0; sp < G::NSPLIT; ++sp)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int j = 0; j < G::MCH; ++j)
+            acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], wf[sp][nt][s], acc[j][nt], 0, 0, 0);
+    }
+    // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nt*16 + li
+#pragma unroll
+    for (int j = 0; j < G::MCH; ++j) {
+      const int jj = ch * G::MCH + j;
+      const int ph = y0 / 2 + 2 * wave + jj / G::MBROW;
+      const int pw = 4 * (jj % G::MBROW) + lq;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const float v0 = acc[j][nt][0], v1 = acc[j][nt][1], v2 = acc[j][nt][2], v3 = acc[j][nt][3];
+        pos += (v0 > 0.f) + (v1 > 0.f) + (v2 > 0.f) + (v3 > 0.f);
+        float mx = v0;
+        uint32_t arg = 0;
+        if (v1 > mx) { mx = v1; arg = 1; }
+        if (v2 > mx) { mx = v2; arg = 2; }
+        if (v3 > mx) { mx = v3; arg = 3; }
+        const size_t o = ((size_t)(img * (G::HO / 2) + ph) * (G::WO / 2) + pw) * G::COUT + nt * 16 + li;
+        a.out[o] = mx > 0.f ? mx * inv255 : 0.f;
+        if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+      }
+    }
+  }
+  if (a.relu_count) relu_count_add(a.relu_count, pos, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// conv0 weight gradient (Conv2DBackpropFilter of conv0, train.py:177 under TF autodiff):
+//   dW[tap, c, o] = (1/255) * sum_{n, pixel p} u8[n, p + tap, c] * dY[n, p, o]
+// with dY the un-pooled output gradient (dP routed to each window's argmax, ReLU folded in).
+// M = (tap, c) = 100 rows (7 m-tiles), N = o (2 n-tiles), K = pixels; dY is split into three
+// bf16 planes (exact), the frames are exact in bf16, so 3 MFMAs per (m-tile, n-tile, 32 px).
+//
+// Persistent workgroups walk bands of RB output rows.  LDS per band:
+//   X: two copies of the RB + 4 input rows, channel-planar bf16, copy h shifted left by h
+//      pixels, so the 8 pixels a lane feeds for tap (kh, kw) start at an even column of copy
+//      kw & 1 (dword aligned);
+//   Y: [split][o][pixel] bf16, o pitch 648 pixels (324 dwords = 4 banks apart: the 16 lanes
+//      of a ds_read_b128 group hit 16 distinct bank quads).
+// K-step s of a band = pixels 32s .. 32s + 31 (row-major over the band), lane group q
+// supplies pixels 32s + 8q .. + 7 (one row, since 80 % 8 == 0); waves take K-steps
+// s = wave, wave + 4, ...  The next band's global loads are issued into registers before
+// the MFMA phase of the current one.  Each wave writes one partial slab (scaled by 1/255).
+// ---------------------------------------------------------------------------------------
+struct Conv0W {
+  static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
+  static constexpr int HO = 80, WO = 80, PH = 40, PW = 40;
+  static constexpr int RB = 8, NBANDS = HO / RB, XROWS = RB + KT - 1;   // 12 rows (<= 84)
+  static constexpr int KPB = RB * WO;              // 640 pixels per band
+  static constexpr int KSTEPS = KPB / 32;          // 20
+  static constexpr int KSW = KSTEPS / 4;           // 5 per wave
+  static constexpr int YP = 648;                   // o pitch (bf16)
+  static constexpr int Y_BF16 = 3 * COUT * YP;
+  static constexpr int XP = 88;                    // row pitch (bf16)
+  static constexpr int XPL = XROWS * XP;           // channel plane
+  static constexpr int XCP = C * XPL;              // copy
+  static constexpr int X_BF16 = 2 * XCP;
+  static constexpr int LDS_U4 = (Y_BF16 + X_BF16) * 2 / 16;
+  static constexpr int MT = 7, M = NTAP * C;
+  static constexpr int NITEM = COUT * (RB / 2) * (PW / 4) / 256;       // dY items per thread
+  static constexpr int NXV = XROWS * WS * C / 16;                      // uint4 of frame rows
+  static_assert(KSTEPS % 4 == 0 && COUT * (RB / 2) * (PW / 4) % 256 == 0 && NXV <= 256, "geom");
+  static_assert(HO % RB == 0 && RB + KT - 1 + HO - RB <= HS, "band rows stay inside the frame");
+};
+
+struct Conv0WArgs {
+  const uint8_t* x;        // frames [B,84,84,4]
+  const float* dp;         // dP0 [B,40,40,32]
+  const uint8_t* code;     // argmax codes of dP0
+  float* part;             // [4 * gridDim.x][100][32] partial slabs
+  int batch;
+};
+
+__global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
+  using G = Conv0W;
+  __shared__ uint4 lds[G::LDS_U4];
+  uint16_t* ys = reinterpret_cast<uint16_t*>(lds);
+  uint16_t* xs = ys + G::Y_BF16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int nbands = a.batch * G::NBANDS;
+
+  // ---- per-thread prefetch registers for one band ----
+  float yv[G::NITEM][4];
+  uint32_t yc[G::NITEM][4];
+  uint4 xv;
+  auto load_band = [&](int band) {
+    const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
+#pragma unroll
+    for (int i = 0; i < G::NITEM; ++i) {
+      const int f = tid + 256 * i, o = f & 31, rest = f >> 5;
+      const int pr = rest / (G::PW / 4), q4 = rest - pr * (G::PW / 4);
+      const size_t base = ((size_t)(img * G::PH + y0 / 2 + pr) * G::PW + 4 * q4) * G::COUT + o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        yv[i][j] = a.dp[base + j * G::COUT];
+        yc[i][j] = a.code[base + j * G::COUT];
+      }
+    }
+    xv = tid < G::NXV ? reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C)[tid]
+                      : make_uint4(0, 0, 0, 0);
+  };
+  auto store_band = [&]() {
+#pragma unroll
+    for (int i = 0; i < G::NITEM; ++i) {
+      const int f = tid + 256 * i, o = f & 31, rest = f >> 5;
+      const int pr = rest / (G::PW / 4), q4 = rest - pr * (G::PW / 4);
+      uint32_t hi[4], mid[4], lo[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) split3(yv[i][j], hi[j], mid[j], lo[j]);
+#pragma unroll
+      for (int sy = 0; sy < 2; ++sy) {
+        // 8 pixels (pooled j, sub-column sx) of un-pooled row 2 pr + sy
+        uint32_t w[3][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t k = yc[i][j];
+          const bool l0 = k == (uint32_t)(2 * sy), l1 = k == (uint32_t)(2 * sy + 1);
+          w[0][j] = (l0 ? hi[j] : 0u) | ((l1 ? hi[j] : 0u) << 16);
+          w[1][j] = (l0 ? mid[j] : 0u) | ((l1 ? mid[j] : 0u) << 16);
+          w[2][j] = (l0 ? lo[j] : 0u) | ((l1 ? lo[j] : 0u) << 16);
+        }
+#pragma unroll
+        for (int sp = 0; sp < 3; ++sp)
+          *reinterpret_cast<uint4*>(ys + (sp * G::COUT + o) * G::YP + (2 * pr + sy) * G::WO + 8 * q4) =
+              make_uint4(w[sp][0], w[sp][1], w[sp][2], w[sp][3]);
+      }
+    }
+    if (tid < G::NXV) {
+      const int p = 4 * tid, r = p / G::WS, x = p - r * G::WS;    // 4 pixels of one row
+      const uint32_t px[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = u8_bf16((px[j] >> (8 * c)) & 255u);
+        uint16_t* p0 = xs + c * G::XPL + r * G::XP + x;              // copy 0
+        *reinterpret_cast<uint2*>(p0) = make_uint2(b[0] | (b[1] << 16), b[2] | (b[3] << 16));
+        uint16_t* p1 = xs + G::XCP + c * G::XPL + r * G::XP + x;     // copy 1: column x - 1
+        if (x > 0) p1[-1] = (uint16_t)b[0];
+        *reinterpret_cast<uint32_t*>(p1) = b[1] | (b[2] << 16);
+        p1[2] = (uint16_t)b[3];
+      }
+    }
+  };
+
+  // per-lane A offsets (bf16 units) for m-tile mt: row m = 16 mt + li = (tap, c)
+  int aoff[G::MT];
+#pragma unroll
+  for (int mt = 0; mt < G::MT; ++mt) {
+    int tap = 4 * mt + (li >> 2);
+    if (tap >= G::NTAP) tap = 0;                       // padded rows: discarded
+    const int c = li & 3, kh = tap / G::KT, kw = tap % G::KT, h = kw & 1;
+    aoff[mt] = h * G::XCP + c * G::XPL + kh * G::XP + (kw - h);
+  }
+  const int yoff = li * G::YP + 8 * lq;                 // + (sp * 32 + 16 nt) * YP + 32 s
+
+  f32x4 acc[G::MT][2];
+#pragma unroll
+  for (int mt = 0; mt < G::MT; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int band = blockIdx.x;
+  if (band < nbands) load_band(band);
+  for (; band < nbands; band += gridDim.x) {
+    __syncthreads();                                   // previous band's LDS reads are done
+    store_band();
+    __syncthreads();
+    if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
+#pragma unroll
+    for (int i = 0; i < G::KSW; ++i) {
+      const int s = wave + 4 * i;
+      const int pb = 32 * s + 8 * lq, r = pb / G::WO, x0 = pb - r * G::WO;
+      const int xo = r * G::XP + x0;
+      bf16x8 av[G::MT];
+#pragma unroll
+      for (int mt = 0; mt < G::MT; ++mt) {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(xs + aoff[mt] + xo);
+        const u32x4 u = {p[0], p[1], p[2], p[3]};
+        av[mt] = __builtin_bit_cast(bf16x8, u);
+      }
+      bf16x8 bv[3][2];
+#pragma unroll
+      for (int sp = 0; sp < 3; ++sp)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const uint4 u = *reinterpret_cast<const uint4*>(ys + (sp * G::COUT + 16 * nt) * G::YP + yoff + 32 * s);
+          bv[sp][nt] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+        }
+#pragma unroll
+      for (int sp = 0; sp < 3; ++sp)
+#pragma unroll
+        for (int mt = 0; mt < G::MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt], bv[sp][nt], acc[mt][nt], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: slab (block, wave); lane holds rows 16 mt + 4 lq + r, column 16 nt + li ----
+  float* pz = a.part + ((size_t)blockIdx.x * 4 + wave) * G::M * G::COUT;
+  const float inv255 = 1.0f / 255.0f;
+#pragma unroll
+  for (int mt = 0; mt < G::MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mt + 4 * lq + r;
+        if (m < G::M) pz[(size_t)m * G::COUT + 16 * nt + li] = acc[mt][nt][r] * inv255;
+      }
+}
+
+}  // namespace ba3c
