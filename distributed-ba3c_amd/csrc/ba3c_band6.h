@@ -1,0 +1,259 @@
+// ba3c_band6.h — band convolutions on bf16 MFMA with fp32-accurate operand splitting.
+//
+// gfx950 has no xf32 and its fp32 MFMA runs at 1/16 of the bf16 rate.  Every fp32 value v is
+// exactly hi + mid + lo with hi, mid, lo bf16 (8 significant bits each, split3 in
+// ba3c_split.h), so for fp32 operands a = a1 + a2 + a3, b = b1 + b2 + b3:
+//
+//   a*b = a1b1 + (a1b2 + a2b1) + (a1b3 + a2b2 + a3b1) + O(2^-24 |a||b|)
+//
+// Each bf16 x bf16 product is exact in fp32 and v_mfma_f32_16x16x32_bf16 accumulates in fp32,
+// so the six products give the convolution at fp32 accuracy (the three dropped terms are
+// below 2^-23 relative — the size of one fp32 rounding) at 16/6 = 2.7x the fp32 MFMA rate.
+//
+// Same band structure as conv_band_kernel (ba3c_conv.h): one workgroup = one image x RB
+// output rows; the input rows the band needs are staged ONCE into LDS — here already split,
+// [row][col][split][CIN] bf16 with a pixel pitch PP and row pitch RP (bytes) chosen by a
+// bank-conflict search (affine, so every MFMA operand read is a ds_read_b128 at a
+// compile-time immediate offset from one per-m-block base).  K-step t = (tap, 32-channel
+// chunk); lane group q supplies channels 8q..8q+7, so a lane's A fragment of one split is
+// 16 contiguous bytes.  B (weights) comes from a per-step [split][N][K] bf16 copy (L2
+// resident) through a register ring.  Pooled epilogues are unchanged: rows are ordered
+// (window, sub) so a lane's 4 accumulator rows are one 2x2 window (16x16 C layout).
+#pragma once
+#include "ba3c_split.h"
+
+namespace ba3c {
+
+// G: BandGeom (ba3c_conv.h).  PP_: pixel pitch in bytes (>= 6 CIN), RPX_: extra row bytes.
+template <class G_, int PP_, int RPX_, int MCH_>
+struct Band6 {
+  using G = G_;
+  static constexpr int PP = PP_, RP = G::WS * PP_ + RPX_, MCH = MCH_;
+  static constexpr int SPB = 2 * G::CIN;                 // bytes per split of a pixel
+  static constexpr int LDS_BYTES = G::SROWS * RP;
+  static constexpr int K32 = G::CIN / 32;                // 32-channel chunks per tap
+  static constexpr int NT = G::KH * G::KW * K32;         // k-steps
+  static constexpr int NCH = (G::MBW + MCH - 1) / MCH;   // m-block chunks per wave
+  static_assert(G::CIN % 32 == 0 && PP % 16 == 0 && RP % 16 == 0 && PP >= 3 * SPB, "band6 layout");
+  static_assert(LDS_BYTES <= 160 * 1024, "band6 LDS");
+};
+
+struct Band6Args {
+  const float* src;        // SRC 0: input map [B,HS,WS,CIN];  SRC 1: dP [B,UPH,UPW,CIN]
+  const uint8_t* code;     // SRC 1: argmax codes of dP
+  const uint16_t* wt6;     // [3][COUT][KH*KW*CIN] bf16 splits (prepared per step)
+  float* out;              // POOL: pooled [B,HO/2,WO/2,COUT]; else [B,HO,WO,COUT]
+  uint8_t* out_code;       // POOL: argmax codes (may be null: predictor)
+  unsigned long long* relu_count;
+  int batch;
+};
+
+template <class L>
+__global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
+  using G = typename L::G;
+  __shared__ uint4 lds4[L::LDS_BYTES / 16];
+  char* lds = reinterpret_cast<char*>(lds4);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.x / G::NBANDS;
+  const int bnd = blockIdx.x - img * G::NBANDS;
+  const int y0 = bnd * G::RB;
+  const int rows_out = min(G::RB, G::HO - y0);
+
+  // ---- stage input rows [y0, y0 + rows_out + KH - 1), split into 3 bf16 planes ----
+  {
+    constexpr int Q = G::CIN / 4;                        // float4 per pixel
+    constexpr int NTOT = (G::SROWS * G::WS * Q + 255) / 256;
+    constexpr int NPT = NTOT < 8 ? NTOT : 8;
+    const int srows = rows_out + G::KH - 1;
+    const int nvec = srows * G::WS * Q;
+    for (int base = 0; base < NTOT; base += NPT) {
+      float4 v[NPT];
+      uint32_t cd[G::SRC == 1 ? NPT : 1];
+      int sub[G::SRC == 1 ? NPT : 1];
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int f = tid + 256 * (base + i);
+        const int pix = f / Q, cq = f - pix * Q;
+        const int ry = pix / G::WS, x = pix - ry * G::WS;
+        const int y = y0 + ry;
+        if constexpr (G::SRC == 0) {
+          v[i] = f < nvec ? *reinterpret_cast<const float4*>(
+                                a.src + ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + cq * 4)
+                          : f4zero();
+        } else {
+          const int uy = y - G::PADY, ux = x - G::PADX;
+          sub[i] = -1;
+          v[i] = f4zero();
+          cd[i] = 0;
+          if (f < nvec && uy >= 0 && uy < G::UHO && ux >= 0 && ux < G::UWO) {
+            const int pidx = img * (G::UPH * G::UPW) + (uy >> 1) * G::UPW + (ux >> 1);
+            v[i] = *reinterpret_cast<const float4*>(a.src + (size_t)pidx * G::CIN + cq * 4);
+            cd[i] = *reinterpret_cast<const uint32_t*>(a.code + (size_t)pidx * G::CIN + cq * 4);
+            sub[i] = ((uy & 1) << 1) | (ux & 1);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int f = tid + 256 * (base + i);
+        if (f < nvec) {
+          const int pix = f / Q, cq = f - pix * Q;
+          const int ry = pix / G::WS, x = pix - ry * G::WS;
+          float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+          if constexpr (G::SRC == 1) {
+            const uint32_t s = (uint32_t)sub[i], c = cd[i];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == s ? e[k] : 0.f;
+          }
+          uint32_t hi[4], mid[4], lo[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) split3(e[k], hi[k], mid[k], lo[k]);
+          char* p = lds + ry * L::RP + x * L::PP + cq * 8;
+          *reinterpret_cast<uint2*>(p) = make_uint2(hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16));
+          *reinterpret_cast<uint2*>(p + L::SPB) = make_uint2(mid[0] | (mid[1] << 16), mid[2] | (mid[3] << 16));
+          *reinterpret_cast<uint2*>(p + 2 * L::SPB) = make_uint2(lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16));
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const int nb = wave % G::NB;
+  const int mb0 = wave / G::NB;
+  const int li = lane & 15, lq = lane >> 4;
+  const int col = nb * 16 + li;
+  // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] bf16
+  const uint16_t* wrow = a.wt6 + (size_t)col * G::KDIM + 8 * lq;
+  constexpr size_t WSPLIT = (size_t)G::COUT * G::KDIM;
+  unsigned long long pos = 0;
+
+#pragma unroll
+  for (int chn = 0; chn < L::NCH; ++chn) {
+    constexpr int MCH = L::MCH;
+    int abase[MCH];                                       // bytes
+    bool live[MCH];
+#pragma unroll
+    for (int j = 0; j < MCH; ++j) {
+      const int mb = mb0 + (chn * MCH + j) * G::WPN;
+      const int row = mb * 16 + li;
+      int oy, ox;
+      if constexpr (G::POOL) {
+        const int w = row >> 2, sb = row & 3;
+        const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
+        oy = 2 * ph + (sb >> 1);
+        ox = 2 * pw + (sb & 1);
+      } else {
+        oy = row / G::WO;
+        ox = row - oy * G::WO;
+      }
+      live[j] = chn * MCH + j < G::MBW && mb < G::MB;
+      const bool ok = live[j] && row < G::MROWS && oy < rows_out;
+      abase[j] = (ok ? oy * L::RP + ox * L::PP : 0) + 16 * lq;
+    }
+    f32x4 acc[MCH];
+#pragma unroll
+    for (int j = 0; j < MCH; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int LA = 2;
+    uint4 bring[LA + 1][3];
+#pragma unroll
+    for (int t = 0; t < LA && t < L::NT; ++t)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wrow + s * WSPLIT + 32 * t);
+#pragma unroll
+    for (int t = 0; t < L::NT; ++t) {
+      if (t + LA < L::NT) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+          bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wrow + s * WSPLIT + 32 * (t + LA));
+      }
+      bf16x8 b[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const uint4 u = bring[t % (LA + 1)][s];
+        b[s] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+      }
+      const int tap = t / L::K32, ch = t - tap * L::K32;
+      const int kh = tap / G::KW, kw = tap - kh * G::KW;
+      const int toff = kh * L::RP + kw * L::PP + ch * 64;
+      bf16x8 av[3][MCH];
+#pragma unroll
+      for (int j = 0; j < MCH; ++j)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * L::SPB);
+          av[s][j] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+        }
+      // a1b1, a1b2, a2b1, a1b3, a2b2, a3b1 — interleaved over m-blocks
+#pragma unroll
+      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][j], b[0], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][j], b[1], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][j], b[0], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][j], b[2], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][j], b[1], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][j], b[0], acc[j], 0, 0, 0);
+    }
+
+    // ---- epilogue (16x16 C layout: lane holds column li, rows 4 lq + r) ----
+#pragma unroll
+    for (int j = 0; j < MCH; ++j) {
+      const int mb = mb0 + (chn * MCH + j) * G::WPN;
+      if (!live[j]) continue;
+      if constexpr (G::POOL) {
+        const int w = mb * 4 + lq;
+        const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
+        const float v0 = acc[j][0], v1 = acc[j][1], v2 = acc[j][2], v3 = acc[j][3];
+        if (w * 4 < G::MROWS && 2 * ph < rows_out) {
+          pos += (v0 > 0.f) + (v1 > 0.f) + (v2 > 0.f) + (v3 > 0.f);
+          float mx = v0;
+          uint32_t arg = 0;
+          if (v1 > mx) { mx = v1; arg = 1; }
+          if (v2 > mx) { mx = v2; arg = 2; }
+          if (v3 > mx) { mx = v3; arg = 3; }
+          const size_t o = ((size_t)(img * (G::HO / 2) + y0 / 2 + ph) * (G::WO / 2) + pw) * G::COUT + col;
+          a.out[o] = fmaxf(mx, 0.f);
+          if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mb * 16 + lq * 4 + r;
+          const int oy = row / G::WO, ox = row - oy * G::WO;
+          if (row < G::MROWS && oy < rows_out)
+            a.out[((size_t)(img * G::HO + y0 + oy) * G::WO + ox) * G::COUT + col] = acc[j][r];
+        }
+      }
+    }
+  }
+  if (G::POOL && a.relu_count) relu_count_add(a.relu_count, pos, lane);
+}
+
+// fp32 [N][K] band-conv weight copies -> [3][N][K] bf16 splits (hi, mid, lo), one region
+// per job; wt6 region of job i starts at 3 * (fp32 offset of job i) bf16 elements.
+struct WSplitArgs {
+  const float* wt;
+  uint16_t* wt6;
+  int off[4], n[4];
+  int njobs;
+};
+
+__global__ void __launch_bounds__(256) wsplit_kernel(const WSplitArgs a) {
+  const int j = blockIdx.y;
+  const float* src = a.wt + a.off[j];
+  uint16_t* dst = a.wt6 + 3 * (size_t)a.off[j];
+  const int n = a.n[j];
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+    uint32_t hi, mid, lo;
+    split3(src[e], hi, mid, lo);
+    dst[e] = (uint16_t)hi;
+    dst[n + e] = (uint16_t)mid;
+    dst[2 * n + e] = (uint16_t)lo;
+  }
+}
+
+}  // namespace ba3c

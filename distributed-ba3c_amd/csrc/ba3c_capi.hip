@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/ba3c.h"
+#include "ba3c_band6.h"
 #include "ba3c_conv.h"
 #include "ba3c_problems.h"
 #include "ba3c_small.h"
@@ -66,6 +67,7 @@ struct ba3c_handle {
   TensorTable table;
   bool band = true;   // band-conv kernels for conv1/conv2 fwd+dgrad (BA3C_GENERIC=1: GEMM engine)
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
+  bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -83,6 +85,11 @@ using GConv1F = BandGeom<40, 40, 32, 32, 5, 5, 6, true, 0, 4>;
 using GConv2F = BandGeom<18, 18, 32, 64, 5, 5, 14, true, 0, 4>;
 using GConv1D = BandGeom<44, 44, 32, 32, 5, 5, 4, false, 1, 8, 4, 4, 18, 18, 36, 36>;
 using GConv2D = BandGeom<22, 22, 64, 32, 5, 5, 6, false, 1, 8, 4, 4, 7, 7, 14, 14>;
+// bf16x6 variants (ba3c_band6.h): pixel pitch / extra row bytes from a bank-conflict search
+using L6Conv1F = Band6<GConv1F, 192, 32, 7>;
+using L6Conv2F = Band6<GConv2F, 192, 32, 7>;
+using L6Conv1D = Band6<GConv1D, 224, 128, 5>;
+using L6Conv2D = Band6<GConv2D, 416, 128, 4>;
 // weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
 using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
 using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
@@ -96,6 +103,7 @@ constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64
 
 struct Workspace {
   float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *sumsq, *wt;
+  uint16_t* wt6;   // [3][N][K] bf16 splits of the four band-conv weight copies
   uint8_t *c0, *c1, *c2;
   unsigned long long* relu;
   size_t bytes;
@@ -160,6 +168,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   w.h = (float*)take(Bz * F * 4);
   w.relu = (unsigned long long*)take(RELU_SLOTS * 8);
   w.wt = (float*)take((size_t)WT_TOTAL * 4);
+  w.wt6 = (uint16_t*)take((size_t)3 * WT_C0F * 2);
   if (train) {
     w.c0 = (uint8_t*)take(Bz * P0);
     w.c1 = (uint8_t*)take(Bz * P1);
@@ -238,6 +247,27 @@ int launch_band(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a) {
   return BA3C_OK;
 }
 
+template <class L>
+int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
+                 int wt_off) {
+  const Band6Args b{a.src, a.code, w.wt6 + 3 * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch};
+  dim3 grid(a.batch * L::G::NBANDS);
+  {
+    ProbeScope ps(h, s, kid);
+    hipLaunchKernelGGL(conv_band6_kernel<L>, grid, dim3(256), 0, s, b);
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+// band conv: bf16x6 split MFMA when enabled, fp32 MFMA otherwise
+template <class L>
+int launch_bandx(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
+                 int wt_off) {
+  if (h->b6) return launch_band6<L>(h, s, kid, a, w, wt_off);
+  return launch_band<typename L::G>(h, s, kid, a);
+}
+
 // persistent weight-gradient band kernel + deterministic reduction into the flat HWIO grads
 template <class G>
 int launch_wgband(ba3c_handle* h, hipStream_t s, int kid, const WgArgs& a, int pmax, float* dst,
@@ -271,6 +301,19 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
   a.njobs = train ? 4 : 2;
   hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
+  if (h->b6) {
+    WSplitArgs sa{};
+    sa.wt = w.wt;
+    sa.wt6 = w.wt6;
+    const int offs[4] = {WT_C1F, WT_C2F, WT_C1D, WT_C2D};
+    for (int j = 0; j < 4; ++j) {
+      sa.off[j] = offs[j];
+      sa.n[j] = a.job[j].n;
+    }
+    sa.njobs = a.njobs;
+    hipLaunchKernelGGL(wsplit_kernel, dim3(64, a.njobs), dim3(256), 0, s, sa);
+    HIP_TRY(hipGetLastError());
+  }
   if (h->cfg.channels == 4 && h->split) {
     hipLaunchKernelGGL(conv0s_wprep_kernel, dim3((2 * Conv0S::KSTEPS * 64 + 255) / 256), dim3(256), 0,
                        s, prm + h->tensors[h->idx_conv[0]].offset,
@@ -320,10 +363,10 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
     }
     if (h->band) {
-      CHECK(launch_band<GConv1F>(h, s, BA3C_K_CONV1_FWD,
-                                 BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}));
-      CHECK(launch_band<GConv2F>(h, s, BA3C_K_CONV2_FWD,
-                                 BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B}));
+      CHECK(launch_bandx<L6Conv1F>(h, s, BA3C_K_CONV1_FWD,
+                                     BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}, w, WT_C1F));
+      CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD,
+                                     BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B}, w, WT_C2F));
     } else {
       ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> c1{w.p0, W1, w.p1, w.c1, rc, 1.0f, B * 1296, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
@@ -339,10 +382,10 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
                                                    B * 6400, 32, 25 * CH, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
     }
-    CHECK(launch_band<GConv1F>(h, s, BA3C_K_CONV1_FWD,
-                               BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}));
-    CHECK(launch_band<GConv2F>(h, s, BA3C_K_CONV2_FWD,
-                               BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B}));
+    CHECK(launch_bandx<L6Conv1F>(h, s, BA3C_K_CONV1_FWD,
+                                   BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}, w, WT_C1F));
+    CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD,
+                                   BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B}, w, WT_C2F));
   } else {
     ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
                                                  B * 6400, 32, 25 * CH, 0};
@@ -436,8 +479,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       CHECK(conv_reduce(pl, 2, 32, 32));
     }
     if (h->band) {
-      CHECK(launch_band<GConv2D>(h, s, BA3C_K_CONV2_DGRAD,
-                                 BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B}));
+      CHECK(launch_bandx<L6Conv2D>(h, s, BA3C_K_CONV2_DGRAD,
+                                     BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B}, w, WT_C2D));
     } else {
       ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
@@ -455,8 +498,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       CHECK(conv_reduce(pl, 1, 32, 32));
     }
     if (h->band) {
-      CHECK(launch_band<GConv1D>(h, s, BA3C_K_CONV1_DGRAD,
-                                 BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B}));
+      CHECK(launch_bandx<L6Conv1D>(h, s, BA3C_K_CONV1_DGRAD,
+                                     BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B}, w, WT_C1D));
     } else {
       ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
@@ -551,6 +594,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   h->cfg = c;
   if (const char* e = getenv("BA3C_GENERIC")) h->band = !(e[0] == '1');
   if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
+  if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
   int64_t off = 0;
