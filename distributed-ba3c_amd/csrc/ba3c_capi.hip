@@ -21,6 +21,7 @@
 #include "ba3c_small.h"
 #include "ba3c_split.h"
 #include "ba3c_wgrad.h"
+#include "ba3c_wgrad6.h"
 
 using namespace ba3c;
 
@@ -68,6 +69,7 @@ struct ba3c_handle {
   bool band = true;   // band-conv kernels for conv1/conv2 fwd+dgrad (BA3C_GENERIC=1: GEMM engine)
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
+  bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -95,6 +97,9 @@ using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
 using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
 using GWg2 = WgGeom<18, 18, 32, 5, 5, 64, 7, false, 2>;
 constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
+using G6Wg1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 224>;
+using G6Wg2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 192>;
+constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workgroups
 constexpr int WG_P0S = 256;   // conv0s_wgrad_kernel: one 141 KB-LDS workgroup per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
               WT_C2D = WT_C1D + 800 * 32, WT_C0F = WT_C2D + 1600 * 32,
@@ -146,6 +151,8 @@ size_t max_partials(const ba3c_handle* h, int B) {
   mx = std::max(mx, (size_t)4 * WG_P0S * Conv0W::M * 32);
   mx = std::max(mx, (size_t)WG_P1 * GWg1::M * 32);
   mx = std::max(mx, (size_t)WG_P2 * GWg2::M * 64);
+  mx = std::max(mx, (size_t)W6_P1 * G6Wg1::M * G6Wg1::COUT);
+  mx = std::max(mx, (size_t)W6_P2 * G6Wg2::M * G6Wg2::COUT);
   return mx;
 }
 
@@ -285,6 +292,25 @@ int launch_wgband(ba3c_handle* h, hipStream_t s, int kid, const WgArgs& a, int p
   mp.N = G::COUT;
   mp.cin = G::CIN;
   mp.cinpad = cinpad;
+  mp.dst = dst;
+  return launch_reduce(h, s, a.part, P, mp);
+}
+
+// bf16x6 weight-gradient kernel + deterministic reduction into the flat HWIO grads
+template <class G>
+int launch_wgrad6(ba3c_handle* h, hipStream_t s, int kid, const Wg6Args& a, int pmax, float* dst) {
+  const int P = std::min(pmax, a.batch * G::NBANDS);
+  {
+    ProbeScope ps(h, s, kid);
+    hipLaunchKernelGGL(wgrad6_kernel<G>, dim3(P, G::NCG * G::NOG), dim3(256), 0, s, a);
+  }
+  HIP_TRY(hipGetLastError());
+  ReduceMap mp{};
+  mp.kind = 0;
+  mp.M = G::M;
+  mp.N = G::COUT;
+  mp.cin = G::CIN;
+  mp.cinpad = G::CIN;
   mp.dst = dst;
   return launch_reduce(h, s, a.part, P, mp);
 }
@@ -469,7 +495,10 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   }
   // conv2
   {
-    if (h->band) {
+    if (h->band && h->w6) {
+      CHECK(launch_wgrad6<G6Wg2>(h, s, BA3C_K_CONV2_WGRAD, Wg6Args{w.p1, w.dp2, w.c2, w.part, B}, W6_P2,
+                                 grads + h->tensors[h->idx_conv[2]].offset));
+    } else if (h->band) {
       CHECK(launch_wgband<GWg2>(h, s, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part, B}, WG_P2,
                                 grads + h->tensors[h->idx_conv[2]].offset, 32));
     } else {
@@ -488,7 +517,10 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   }
   // conv1
   {
-    if (h->band) {
+    if (h->band && h->w6) {
+      CHECK(launch_wgrad6<G6Wg1>(h, s, BA3C_K_CONV1_WGRAD, Wg6Args{w.p0, w.dp1, w.c1, w.part, B}, W6_P1,
+                                 grads + h->tensors[h->idx_conv[1]].offset));
+    } else if (h->band) {
       CHECK(launch_wgband<GWg1>(h, s, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part, B}, WG_P1,
                                 grads + h->tensors[h->idx_conv[1]].offset, 32));
     } else {
@@ -595,6 +627,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_GENERIC")) h->band = !(e[0] == '1');
   if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
+  if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
   int64_t off = 0;

@@ -1,0 +1,247 @@
+// ba3c_wgrad6.h — weight gradients of conv1/conv2 (Conv2DBackpropFilter, train.py:187-204
+// under TF autodiff, train/multigpu.py:85-86) on bf16 MFMA with fp32-accurate splitting.
+//
+//   dW[kh,kw,c,o] = sum_{n,y,x} X[n, y+kh, x+kw, c] * dY[n, y, x, o]
+//
+// GEMM view: M = (tap, c), N = o, K = output pixels.  X and dY are fp32; each is split into
+// three bf16 planes (hi + mid + lo == value exactly, split3x2) and the six significant
+// cross products (a1b1, a1b2, a2b1, a1b3, a2b2, a3b1) run on v_mfma_f32_16x16x32_bf16 with
+// fp32 accumulation (dropped terms < 2^-23 relative: fp32 accuracy, see ba3c_band6.h).
+//
+// Persistent workgroups walk bands (image, RB output rows); blockIdx.y selects a group of
+// CW input channels x OW output channels, so one workgroup's LDS holds
+//   X  [XROWS][WS][split][CW]  bf16, pixel pitch PX bytes  (the band's input rows + 4)
+//   dY [KPAD][split][OW]       bf16, pixel pitch PY bytes  (un-pooled: dP routed to each
+//                                                         window's argmax, ReLU folded in)
+// with dY's pixels compacted (p = y*WO + x: no MFMA spent on the WS - WO dead columns) and
+// zero-padded to a multiple of 32.  Both operands have K = pixels on the LDS row axis, so
+// they are read with ds_read_b64_tr_b16 (hardware transpose: 4 pixel rows x 16 channel
+// columns per 16-lane group).  Within a k-step the 32 pixels are permuted so the 8 rows a
+// 32-lane half reads are consecutive pixels: with PX = 3*32 and PY = 7*32 bytes those land
+// in 8 distinct 32-byte bank slots (conflict-free except where a run wraps a row of X).
+// Each lane's address is per k-step (compacted pixel -> (y, x)); the tap offset is an
+// immediate.  Accumulators stay in registers across all bands; one fp32 partial slab per
+// workgroup, reduced deterministically by wgrad_reduce_kernel.
+#pragma once
+#include "ba3c_split.h"
+
+namespace ba3c {
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// RNE fp32 pair -> packed bf16 pair (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
+}
+// (a, b) = hi + mid + lo exactly, each a packed bf16 pair (RNE at every stage)
+__device__ __forceinline__ void split3x2(float a, float b, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+  hi = pack_bf16x2(a, b);
+  const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xFFFF0000u);
+  mid = pack_bf16x2(ra, rb);
+  const float sa = ra - __uint_as_float(mid << 16), sb = rb - __uint_as_float(mid & 0xFFFF0000u);
+  lo = pack_bf16x2(sa, sb);
+}
+
+__device__ __forceinline__ uint2 lds_tr16(const char* p) {
+  const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) i16x4*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
+template <int HS_, int WS_, int CIN_, int COUT_, int RB_, int CW_, int OW_, int PX_, int PY_>
+struct Wg6Geom {
+  static constexpr int HS = HS_, WS = WS_, CIN = CIN_, COUT = COUT_, RB = RB_, CW = CW_, OW = OW_;
+  static constexpr int KH = 5, KW = 5, NTAP = 25;
+  static constexpr int HO = HS - KH + 1, WO = WS - KW + 1, PH = HO / 2, PW = WO / 2;
+  static constexpr int NBANDS = (HO + RB - 1) / RB;
+  static constexpr int KP = RB * WO;                      // output pixels of a full band
+  static constexpr int KS = (KP + 31) / 32, KPAD = 32 * KS;
+  static constexpr int XROWS = RB + KH - 1;
+  static constexpr int PX = PX_, PY = PY_;                // pixel pitches (bytes)
+  static constexpr int XSB = 2 * CW, YSB = 2 * OW;        // bytes per split
+  static constexpr int X_BYTES = XROWS * WS * PX, Y_BYTES = KPAD * PY;
+  static constexpr int NCG = CIN / CW, NOG = COUT / OW;
+  static constexpr int TAPS0 = (NTAP + 1) / 2;            // taps of wave half 0 (13), half 1: 12
+  static constexpr int M = NTAP * CIN;
+  static_assert(CW == 16 && OW == 32, "16 input x 32 output channels per workgroup");
+  static_assert(PX >= 3 * XSB && PY >= 3 * YSB && PX % 8 == 0 && PY % 8 == 0, "pitches");
+  static_assert(X_BYTES % 16 == 0 && RB % 2 == 0, "wgrad6 geometry");
+};
+
+struct Wg6Args {
+  const float* x;          // X [B,HS,WS,CIN] pooled fp32 map
+  const float* dp;         // dP [B,PH,PW,COUT]
+  const uint8_t* code;     // argmax codes of dP (255 = no gradient)
+  float* part;             // [gridDim.x][M][COUT] partial slabs
+  int batch;
+};
+
+template <class G>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wgrad6_kernel(const Wg6Args a) {
+  __shared__ uint4 lds4[(G::X_BYTES + G::Y_BYTES) / 16];
+  char* xs = reinterpret_cast<char*>(lds4);
+  char* ys = xs + G::X_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cg = blockIdx.y / G::NOG, og = blockIdx.y - cg * G::NOG;
+  const int c0 = cg * G::CW, o0 = og * G::OW;
+  const int nb = wave & 1, th = wave >> 1;
+  const int tap0 = th * G::TAPS0;
+  constexpr int T0 = G::TAPS0, T1 = G::NTAP - G::TAPS0;
+
+  // tr-read lane roles: group g = lane >> 4, row q, column quad p
+  const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+  const int kperm = 16 * (g >> 1) + 4 * (g & 1) + q;      // + 8 r for read r
+
+  f32x4 acc[T0];
+#pragma unroll
+  for (int t = 0; t < T0; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- staging work per thread ----
+  constexpr int XQ = G::CW / 4;                           // float4 per X pixel (4)
+  constexpr int XN = G::XROWS * G::WS * XQ;
+  constexpr int XPT = (XN + 255) / 256;
+  constexpr int YQ = G::OW / 4;                           // float4 per dY pixel (8)
+  constexpr int YN = G::KPAD * YQ;
+  constexpr int YPT = (YN + 255) / 256;
+  float4 xv[XPT], yv[YPT];
+  uint32_t yc[YPT];
+  int ysub[YPT];
+
+  const int nbands = a.batch * G::NBANDS;
+  auto load_band = [&](int band) {
+    const int img = band / G::NBANDS;
+    const int y0 = (band - img * G::NBANDS) * G::RB;
+    const int rows_out = min(G::RB, G::HO - y0);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int f = tid + 256 * i;
+      const int pix = f / XQ, cq = f - pix * XQ;
+      const int ry = pix / G::WS, x = pix - ry * G::WS;
+      const int y = y0 + ry;
+      xv[i] = f4zero();
+      if (f < XN && y < G::HS)
+        xv[i] = *reinterpret_cast<const float4*>(a.x + ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + c0 + cq * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + 256 * i;
+      const int p = f / YQ, oq = f - p * YQ;
+      const int ry = p / G::WO, x = p - ry * G::WO;
+      yv[i] = f4zero();
+      yc[i] = 0;
+      ysub[i] = -1;
+      if (f < YN && ry < rows_out) {
+        const int y = y0 + ry;
+        const size_t pidx = (size_t)(img * G::PH + (y >> 1)) * G::PW + (x >> 1);
+        yv[i] = *reinterpret_cast<const float4*>(a.dp + pidx * G::COUT + o0 + oq * 4);
+        yc[i] = *reinterpret_cast<const uint32_t*>(a.code + pidx * G::COUT + o0 + oq * 4);
+        ysub[i] = ((y & 1) << 1) | (x & 1);
+      }
+    }
+  };
+  auto store_band = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int f = tid + 256 * i;
+      if (f < XN) {
+        const int pix = f / XQ, cq = f - pix * XQ;
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3x2(xv[i].x, xv[i].y, h0, m0, l0);
+        split3x2(xv[i].z, xv[i].w, h1, m1, l1);
+        char* p = xs + pix * G::PX + cq * 8;
+        *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(p + G::XSB) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(p + 2 * G::XSB) = make_uint2(l0, l1);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + 256 * i;
+      if (f < YN) {
+        const int p = f / YQ, oq = f - p * YQ;
+        const uint32_t s = (uint32_t)ysub[i], c = yc[i];
+        float e[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == s ? e[k] : 0.f;
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3x2(e[0], e[1], h0, m0, l0);
+        split3x2(e[2], e[3], h1, m1, l1);
+        char* d = ys + p * G::PY + oq * 8;
+        *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(d + G::YSB) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(d + 2 * G::YSB) = make_uint2(l0, l1);
+      }
+    }
+  };
+
+  int band = blockIdx.x;
+  if (band < nbands) load_band(band);
+  for (; band < nbands; band += gridDim.x) {
+    const int img = band / G::NBANDS;
+    const int rows_out = min(G::RB, G::HO - (band - img * G::NBANDS) * G::RB);
+    const int kvalid = rows_out * G::WO;
+    __syncthreads();                                      // previous band's LDS reads done
+    store_band();
+    __syncthreads();
+    if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
+
+#pragma unroll 1
+    for (int s = 0; s < G::KS; ++s) {
+      // this lane's pixel rows for tr reads r = 0, 1
+      int xb[2], yb[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        int p = 32 * s + kperm + 8 * r;
+        yb[r] = p * G::PY + nb * 32 + 8 * pq;
+        if (p >= kvalid) p = 0;                           // padded pixels: dY is zero
+        const int y = p / G::WO, x = p - y * G::WO;
+        xb[r] = (y * G::WS + x) * G::PX + 8 * pq;
+      }
+      bf16x8 b[3];
+#pragma unroll
+      for (int sp = 0; sp < 3; ++sp) {
+        const uint2 u0 = lds_tr16(ys + yb[0] + sp * G::YSB);
+        const uint2 u1 = lds_tr16(ys + yb[1] + sp * G::YSB);
+        b[sp] = as_bf16x8(u0, u1);
+      }
+#pragma unroll
+      for (int t = 0; t < T0; ++t) {
+        if (th == 1 && t >= T1) break;
+        const int tap = tap0 + t;
+        const int kh = tap / G::KW, kw = tap - kh * G::KW;
+        const int toff = (kh * G::WS + kw) * G::PX;
+        bf16x8 av[3];
+#pragma unroll
+        for (int sp = 0; sp < 3; ++sp) {
+          const uint2 u0 = lds_tr16(xs + xb[0] + toff + sp * G::XSB);
+          const uint2 u1 = lds_tr16(xs + xb[1] + toff + sp * G::XSB);
+          av[sp] = as_bf16x8(u0, u1);
+        }
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[0], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[1], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[0], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[2], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[1], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], b[0], acc[t], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: C layout 16x16: lane holds column (lane & 15) = o, rows 4*(lane>>4)+r = c ----
+  float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
+  const int o = o0 + nb * 16 + (lane & 15);
+#pragma unroll
+  for (int t = 0; t < T0; ++t) {
+    if (th == 1 && t >= T1) break;
+    const int tap = tap0 + t;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = c0 + 4 * (lane >> 4) + r;
+      pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[t][r];
+    }
+  }
+}
+
+}  // namespace ba3c
