@@ -25,6 +25,26 @@ sys.path.insert(0, ROOT)
 
 METRIC = "BA3C train-step samples/sec, 84x84x4 frames, batch 32 & 2048, at 1/2/4/8 GPUs"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (16 x the fp32 rate)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def kernel_peak(split):
+    """Ceiling of a kernel in algorithmic fp32 TFLOP/s given its arithmetic path: fp32 MFMA,
+    or a bf16 split issuing `split` bf16 products per fp32 product (ba3c_kernel_split)."""
+    return FP32_MFMA_PEAK_TFLOPS if split <= 1 else BF16_MFMA_PEAK_TFLOPS / split
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    (scripts/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md §HBM), or None if it was not collected for this kernel."""
+    try:
+        d = json.load(open(PMC_TRAFFIC))
+    except (OSError, ValueError):
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None or "hbm_bytes" not in k else int(k["hbm_bytes"])
 
 # algorithmic MAC per sample of each layer's forward product (real C input channels;
 # SURVEY.md §8d), backward kernels of a layer do the same algorithmic work
@@ -257,11 +277,18 @@ def main():
     avg_ms = probe_ms / max(launches, 1)
     roof = None
     if dom_flops:
+        split = tr.engine.kernel_split(dom)
+        peak = kernel_peak(split)
         ach = dom_flops / (avg_ms / 1000.0) / 1e12
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
-                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "avg_launch_ms": round(avg_ms, 4), "launches": launches}
+                "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                "traffic": pmc_traffic(dom), "avg_launch_ms": round(avg_ms, 4),
+                "launches": launches,
+                "path": "fp32 MFMA" if split <= 1 else
+                        "bf16 MFMA, %d products per fp32 product (exact split)" % split,
+                "peak_basis": "algorithmic fp32 FLOP/s: %s" % (
+                    "fp32 MFMA 157.3 TF" if split <= 1 else
+                    "2516.6 TF dense bf16 / %d split products" % split)}
     step_tflops = train_step_flops(B, C, F, A) / (ms_step / 1000.0) / 1e12
 
     out = {"metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
@@ -275,7 +302,8 @@ def main():
                       "global_batch": world * B, "per_gpu_batch": B, "fc_neurons": F,
                       "fc_splits": S, "num_actions": A, "parallelism": "dp%d" % world},
            "step_tflops_algorithmic": round(step_tflops, 2),
-           "step_mfma_frac": round(step_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+           "step_frac_of_bf16x6_peak": round(step_tflops / kernel_peak(6), 4),
+           "step_vs_fp32_mfma_peak": round(step_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
            "roofline": roof,
            "kernel_ms_one_step": {k: round(v, 4) for k, v in per_kernel.items()}}
 

@@ -194,6 +194,11 @@ class Ba3cEngine(object):
         kid = -1 if kernel is None else _lib.KERNEL_IDS[kernel]
         _lib.check(self.lib.ba3c_probe_enable(self.h, kid))
 
+    def kernel_split(self, kernel):
+        """bf16 MFMA products per fp32 product of `kernel` on this handle (6: bf16x6 split,
+        3: conv0's u8 x bf16x3 split, 1: fp32 MFMA, 0: no matrix work)."""
+        return int(self.lib.ba3c_kernel_split(self.h, _lib.KERNEL_IDS[kernel]))
+
     def probe_read(self):
         ms, n = ctypes.c_double(), ctypes.c_int32()
         _lib.check(self.lib.ba3c_probe_read(self.h, ctypes.byref(ms), ctypes.byref(n)))

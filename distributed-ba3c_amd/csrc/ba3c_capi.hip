@@ -899,6 +899,26 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id) {
   return BA3C_OK;
 }
 
+int ba3c_kernel_split(const ba3c_handle* h, int32_t kid) {
+  if (!h || kid < 0 || kid >= BA3C_NUM_KERNELS) return -1;
+  const bool c4 = h->cfg.channels == 4;
+  switch (kid) {
+    case BA3C_K_CONV0_FWD:
+    case BA3C_K_CONV0_WGRAD: return (h->band && c4 && h->split) ? 3 : 1;
+    case BA3C_K_CONV1_FWD:
+    case BA3C_K_CONV2_FWD:
+    case BA3C_K_CONV1_DGRAD:
+    case BA3C_K_CONV2_DGRAD: return (h->band && h->b6) ? 6 : 1;
+    case BA3C_K_CONV1_WGRAD:
+    case BA3C_K_CONV2_WGRAD: return (h->band && h->w6) ? 6 : 1;
+    case BA3C_K_HEADS:
+    case BA3C_K_WGRAD_REDUCE:
+    case BA3C_K_CLIP:
+    case BA3C_K_UPDATE: return 0;
+    default: return 1;
+  }
+}
+
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches) {
   if (!h) return fail(BA3C_ERR_INVALID, "null handle");
   for (int i = 0; i < h->probe_used; ++i) {

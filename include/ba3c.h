@@ -172,6 +172,12 @@ int ba3c_sample(void* stream, const float* probs, const double* u, int32_t batch
 int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
 
+/* Arithmetic path of kernel `kernel_id` on this handle (for roofline accounting; no
+ * reference counterpart): the number of bf16 MFMA products it issues per fp32 product —
+ * 6 for the bf16x6 split (fp32-accurate), 3 for conv0's exact u8 x bf16x3 split — or 1 for
+ * fp32 MFMA (v_mfma_f32_*_f32), 0 for a kernel with no matrix work; -1 on a bad id. */
+int ba3c_kernel_split(const ba3c_handle* h, int32_t kernel_id);
+
 #ifdef __cplusplus
 }
 #endif

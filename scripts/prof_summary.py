@@ -25,6 +25,9 @@ def short(name):
 
 def main():
     rows = list(csv.DictReader(open(summary_csv(sys.argv[1]))))
+    for r in rows:   # rocpd2summary vs rocprofv3 --output-format csv column names
+        r.setdefault("Duration (Nsec)", r.get("TotalDurationNs"))
+        r.setdefault("Average (Nsec)", r.get("AverageNs"))
     total = sum(float(r["Duration (Nsec)"]) for r in rows)
     title = sys.argv[2] if len(sys.argv) > 2 else os.path.basename(sys.argv[1])
     print("# %s\n" % title)
