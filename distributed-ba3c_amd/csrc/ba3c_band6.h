@@ -24,17 +24,25 @@
 
 namespace ba3c {
 
-// G: BandGeom (ba3c_conv.h).  PP_: pixel pitch in bytes (>= 6 CIN), RPX_: extra row bytes.
-template <class G_, int PP_, int RPX_, int MCH_>
+// G: BandGeom (ba3c_conv.h).  PP_: pixel pitch in bytes (>= 6 KPH), RPX_: extra row bytes,
+// MCH_: m-blocks per accumulator chunk, KPH_: input channels staged per phase (0 = all CIN).
+// With KPH < CIN the band is staged in CIN/KPH channel phases through the same LDS (smaller
+// footprint => more workgroups per CU to hide the staging); accumulators persist across
+// phases, so a phased layout needs all of a wave's m-blocks in one chunk.
+template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0>
 struct Band6 {
   using G = G_;
+  static constexpr int KPH = KPH_ ? KPH_ : G_::CIN;
+  static constexpr int NPH = G_::CIN / KPH;
   static constexpr int PP = PP_, RP = G::WS * PP_ + RPX_, MCH = MCH_;
-  static constexpr int SPB = 2 * G::CIN;                 // bytes per split of a pixel
+  static constexpr int SPB = 2 * KPH;                    // bytes per split of a pixel
   static constexpr int LDS_BYTES = G::SROWS * RP;
-  static constexpr int K32 = G::CIN / 32;                // 32-channel chunks per tap
-  static constexpr int NT = G::KH * G::KW * K32;         // k-steps
+  static constexpr int K32 = KPH / 32;                   // 32-channel chunks per tap and phase
+  static constexpr int NT = G::KH * G::KW * K32;         // k-steps per phase
   static constexpr int NCH = (G::MBW + MCH - 1) / MCH;   // m-block chunks per wave
-  static_assert(G::CIN % 32 == 0 && PP % 16 == 0 && RP % 16 == 0 && PP >= 3 * SPB, "band6 layout");
+  static_assert(KPH % 32 == 0 && G::CIN % KPH == 0 && PP % 16 == 0 && RP % 16 == 0 &&
+                PP >= 3 * SPB, "band6 layout");
+  static_assert(NPH == 1 || NCH == 1, "phased staging keeps every accumulator live");
   static_assert(LDS_BYTES <= 160 * 1024, "band6 LDS");
 };
 
@@ -59,9 +67,11 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
   const int y0 = bnd * G::RB;
   const int rows_out = min(G::RB, G::HO - y0);
 
-  // ---- stage input rows [y0, y0 + rows_out + KH - 1), split into 3 bf16 planes ----
-  {
-    constexpr int Q = G::CIN / 4;                        // float4 per pixel
+  // ---- stage input rows [y0, y0 + rows_out + KH - 1), channels of phase ph, split into
+  // three bf16 planes ----
+  auto stage = [&](int ph) {
+    constexpr int Q = L::KPH / 4;                        // float4 per pixel and phase
+    const int cb = ph * L::KPH;
     constexpr int NTOT = (G::SROWS * G::WS * Q + 255) / 256;
     constexpr int NPT = NTOT < 8 ? NTOT : 8;
     const int srows = rows_out + G::KH - 1;
@@ -78,7 +88,7 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
         const int y = y0 + ry;
         if constexpr (G::SRC == 0) {
           v[i] = f < nvec ? *reinterpret_cast<const float4*>(
-                                a.src + ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + cq * 4)
+                                a.src + ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + cb + cq * 4)
                           : f4zero();
         } else {
           const int uy = y - G::PADY, ux = x - G::PADX;
@@ -87,8 +97,8 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
           cd[i] = 0;
           if (f < nvec && uy >= 0 && uy < G::UHO && ux >= 0 && ux < G::UWO) {
             const int pidx = img * (G::UPH * G::UPW) + (uy >> 1) * G::UPW + (ux >> 1);
-            v[i] = *reinterpret_cast<const float4*>(a.src + (size_t)pidx * G::CIN + cq * 4);
-            cd[i] = *reinterpret_cast<const uint32_t*>(a.code + (size_t)pidx * G::CIN + cq * 4);
+            v[i] = *reinterpret_cast<const float4*>(a.src + (size_t)pidx * G::CIN + cb + cq * 4);
+            cd[i] = *reinterpret_cast<const uint32_t*>(a.code + (size_t)pidx * G::CIN + cb + cq * 4);
             sub[i] = ((uy & 1) << 1) | (ux & 1);
           }
         }
@@ -105,18 +115,21 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == s ? e[k] : 0.f;
           }
-          uint32_t hi[4], mid[4], lo[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) split3(e[k], hi[k], mid[k], lo[k]);
+          uint32_t h0, m0, l0, h1, m1, l1;
+          split3x2(e[0], e[1], h0, m0, l0);
+          split3x2(e[2], e[3], h1, m1, l1);
           char* p = lds + ry * L::RP + x * L::PP + cq * 8;
-          *reinterpret_cast<uint2*>(p) = make_uint2(hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16));
-          *reinterpret_cast<uint2*>(p + L::SPB) = make_uint2(mid[0] | (mid[1] << 16), mid[2] | (mid[3] << 16));
-          *reinterpret_cast<uint2*>(p + 2 * L::SPB) = make_uint2(lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16));
+          *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
+          *reinterpret_cast<uint2*>(p + L::SPB) = make_uint2(m0, m1);
+          *reinterpret_cast<uint2*>(p + 2 * L::SPB) = make_uint2(l0, l1);
         }
       }
     }
+  };
+  if constexpr (L::NPH == 1) {
+    stage(0);
+    __syncthreads();
   }
-  __syncthreads();
 
   const int nb = wave % G::NB;
   const int mb0 = wave / G::NB;
@@ -125,6 +138,8 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
   // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] bf16
   const uint16_t* wrow = a.wt6 + (size_t)col * G::KDIM + 8 * lq;
   constexpr size_t WSPLIT = (size_t)G::COUT * G::KDIM;
+  // K index (tap, channel) of k-step t of a phase, relative to the phase's first channel
+  auto koff = [](int t) { return (t / L::K32) * G::CIN + (t % L::K32) * 32; };
   unsigned long long pos = 0;
 
 #pragma unroll
@@ -154,18 +169,26 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
 #pragma unroll
     for (int j = 0; j < MCH; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+#pragma unroll 1
+    for (int ph = 0; ph < L::NPH; ++ph) {
+    if constexpr (L::NPH > 1) {
+      if (ph) __syncthreads();                            // previous phase's reads are done
+      stage(ph);
+      __syncthreads();
+    }
+    const uint16_t* wph = wrow + ph * L::KPH;
     constexpr int LA = 2;
     uint4 bring[LA + 1][3];
 #pragma unroll
     for (int t = 0; t < LA && t < L::NT; ++t)
 #pragma unroll
-      for (int s = 0; s < 3; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wrow + s * WSPLIT + 32 * t);
+      for (int s = 0; s < 3; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
 #pragma unroll
     for (int t = 0; t < L::NT; ++t) {
       if (t + LA < L::NT) {
 #pragma unroll
         for (int s = 0; s < 3; ++s)
-          bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wrow + s * WSPLIT + 32 * (t + LA));
+          bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t + LA));
       }
       bf16x8 b[3];
 #pragma unroll
@@ -197,6 +220,7 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
       for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][j], b[1], acc[j], 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][j], b[0], acc[j], 0, 0, 0);
+    }
     }
 
     // ---- epilogue (16x16 C layout: lane holds column li, rows 4 lq + r) ----

@@ -43,6 +43,7 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kWgradTargetBlocks = 1024;
 constexpr int kMaxBatch = 16384;
+constexpr int kNumCUs = 256;   // MI355X: 8 XCDs x 32 CUs
 
 inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -91,7 +92,7 @@ using GConv2D = BandGeom<22, 22, 64, 32, 5, 5, 6, false, 1, 8, 4, 4, 7, 7, 14, 1
 using L6Conv1F = Band6<GConv1F, 192, 32, 7>;
 using L6Conv2F = Band6<GConv2F, 192, 32, 7>;
 using L6Conv1D = Band6<GConv1D, 224, 128, 5>;
-using L6Conv2D = Band6<GConv2D, 416, 128, 4>;
+using L6Conv2D = Band6<GConv2D, 224, 128, 4, 32>;   // two 32-channel phases
 // weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
 using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
 using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;

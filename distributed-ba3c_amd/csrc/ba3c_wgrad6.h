@@ -28,22 +28,6 @@
 namespace ba3c {
 
 typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-
-// RNE fp32 pair -> packed bf16 pair (v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));
-}
-// (a, b) = hi + mid + lo exactly, each a packed bf16 pair (RNE at every stage)
-__device__ __forceinline__ void split3x2(float a, float b, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
-  hi = pack_bf16x2(a, b);
-  const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xFFFF0000u);
-  mid = pack_bf16x2(ra, rb);
-  const float sa = ra - __uint_as_float(mid << 16), sb = rb - __uint_as_float(mid & 0xFFFF0000u);
-  lo = pack_bf16x2(sa, sb);
-}
-
 __device__ __forceinline__ uint2 lds_tr16(const char* p) {
   const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) i16x4*)(p));
