@@ -54,6 +54,7 @@ struct Band6Args {
   uint8_t* out_code;       // POOL: argmax codes (may be null: predictor)
   unsigned long long* relu_count;
   int batch;
+  int dbg;                 // profiling only: bit0 skip staging loads, bit1 skip the MFMA loop
 };
 
 template <class L>
@@ -69,56 +70,59 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
 
   // ---- stage input rows [y0, y0 + rows_out + KH - 1), channels of phase ph, split into
   // three bf16 planes ----
+  // Index math is 32-bit from per-workgroup base pointers (the band of an SRC 0 map is one
+  // contiguous run of rows); unsigned division by the compile-time Q / WS is a mul-hi.
   auto stage = [&](int ph) {
-    constexpr int Q = L::KPH / 4;                        // float4 per pixel and phase
+    constexpr unsigned Q = L::KPH / 4;                   // float4 per pixel and phase
     const int cb = ph * L::KPH;
     constexpr int NTOT = (G::SROWS * G::WS * Q + 255) / 256;
     constexpr int NPT = NTOT < 8 ? NTOT : 8;
-    const int srows = rows_out + G::KH - 1;
-    const int nvec = srows * G::WS * Q;
+    const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * Q;
+    const float* srcb = G::SRC == 0 ? a.src + ((size_t)(img * G::HS + y0) * G::WS) * G::CIN + cb
+                                    : a.src + (size_t)img * (G::UPH * G::UPW) * G::CIN + cb;
+    const uint8_t* codeb = G::SRC == 1 ? a.code + (size_t)img * (G::UPH * G::UPW) * G::CIN + cb : nullptr;
     for (int base = 0; base < NTOT; base += NPT) {
       float4 v[NPT];
       uint32_t cd[G::SRC == 1 ? NPT : 1];
-      int sub[G::SRC == 1 ? NPT : 1];
+      uint32_t sub[G::SRC == 1 ? NPT : 1];
 #pragma unroll
       for (int i = 0; i < NPT; ++i) {
-        const int f = tid + 256 * (base + i);
-        const int pix = f / Q, cq = f - pix * Q;
-        const int ry = pix / G::WS, x = pix - ry * G::WS;
-        const int y = y0 + ry;
+        const unsigned f = tid + 256u * (base + i);
+        const unsigned pix = f / Q, cq = f - pix * Q;
+        v[i] = f4zero();
+        if (a.dbg & 1) continue;
         if constexpr (G::SRC == 0) {
-          v[i] = f < nvec ? *reinterpret_cast<const float4*>(
-                                a.src + ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + cb + cq * 4)
-                          : f4zero();
+          if (f < nvec) v[i] = *reinterpret_cast<const float4*>(srcb + pix * G::CIN + cq * 4);
         } else {
-          const int uy = y - G::PADY, ux = x - G::PADX;
-          sub[i] = -1;
-          v[i] = f4zero();
+          const unsigned ry = pix / G::WS, x = pix - ry * G::WS;
+          const int uy = (int)(y0 + ry) - G::PADY, ux = (int)x - G::PADX;
+          sub[i] = 4u;                                     // matches no code
           cd[i] = 0;
-          if (f < nvec && uy >= 0 && uy < G::UHO && ux >= 0 && ux < G::UWO) {
-            const int pidx = img * (G::UPH * G::UPW) + (uy >> 1) * G::UPW + (ux >> 1);
-            v[i] = *reinterpret_cast<const float4*>(a.src + (size_t)pidx * G::CIN + cb + cq * 4);
-            cd[i] = *reinterpret_cast<const uint32_t*>(a.code + (size_t)pidx * G::CIN + cb + cq * 4);
+          if (f < nvec && (unsigned)uy < (unsigned)G::UHO && (unsigned)ux < (unsigned)G::UWO) {
+            const unsigned off = ((uy >> 1) * G::UPW + (ux >> 1)) * G::CIN + cq * 4;
+            v[i] = *reinterpret_cast<const float4*>(srcb + off);
+            cd[i] = *reinterpret_cast<const uint32_t*>(codeb + off);
             sub[i] = ((uy & 1) << 1) | (ux & 1);
           }
         }
       }
 #pragma unroll
       for (int i = 0; i < NPT; ++i) {
-        const int f = tid + 256 * (base + i);
+        const unsigned f = tid + 256u * (base + i);
         if (f < nvec) {
-          const int pix = f / Q, cq = f - pix * Q;
-          const int ry = pix / G::WS, x = pix - ry * G::WS;
+          const unsigned pix = f / Q, cq = f - pix * Q;
+          const unsigned ry = pix / G::WS;
           float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
           if constexpr (G::SRC == 1) {
-            const uint32_t s = (uint32_t)sub[i], c = cd[i];
+            const uint32_t sb = sub[i], c = cd[i];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == s ? e[k] : 0.f;
+            for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == sb ? e[k] : 0.f;
           }
           uint32_t h0, m0, l0, h1, m1, l1;
           split3x2(e[0], e[1], h0, m0, l0);
           split3x2(e[2], e[3], h1, m1, l1);
-          char* p = lds + ry * L::RP + x * L::PP + cq * 8;
+          // ry * RP + x * PP == pix * PP + ry * (RP - WS * PP)
+          char* p = lds + pix * L::PP + ry * (L::RP - G::WS * L::PP) + cq * 8;
           *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
           *reinterpret_cast<uint2*>(p + L::SPB) = make_uint2(m0, m1);
           *reinterpret_cast<uint2*>(p + 2 * L::SPB) = make_uint2(l0, l1);
@@ -183,6 +187,7 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
     for (int t = 0; t < LA && t < L::NT; ++t)
 #pragma unroll
       for (int s = 0; s < 3; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
+    if (a.dbg & 2) continue;
 #pragma unroll
     for (int t = 0; t < L::NT; ++t) {
       if (t + LA < L::NT) {

@@ -70,7 +70,8 @@ struct ba3c_handle {
   bool band = true;   // band-conv kernels for conv1/conv2 fwd+dgrad (BA3C_GENERIC=1: GEMM engine)
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
-  bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  bool w6 = true;
+  int dbg = 0;        // BA3C_DBG: profiling-only kernel ablations (results are wrong when set)     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -258,7 +259,8 @@ int launch_band(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a) {
 template <class L>
 int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
                  int wt_off) {
-  const Band6Args b{a.src, a.code, w.wt6 + 3 * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch};
+  const Band6Args b{a.src, a.code, w.wt6 + 3 * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch,
+                    h->dbg};
   dim3 grid(a.batch * L::G::NBANDS);
   {
     ProbeScope ps(h, s, kid);
@@ -629,6 +631,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
+  if (const char* e = getenv("BA3C_DBG")) h->dbg = atoi(e);
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
   int64_t off = 0;
