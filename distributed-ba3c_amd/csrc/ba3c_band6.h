@@ -63,8 +63,9 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
   __shared__ uint4 lds4[L::LDS_BYTES / 16];
   char* lds = reinterpret_cast<char*>(lds4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int img = blockIdx.x / G::NBANDS;
-  const int bnd = blockIdx.x - img * G::NBANDS;
+  const int bid = blockIdx.x;
+  const int img = bid / G::NBANDS;
+  const int bnd = bid - img * G::NBANDS;
   const int y0 = bnd * G::RB;
   const int rows_out = min(G::RB, G::HO - y0);
 

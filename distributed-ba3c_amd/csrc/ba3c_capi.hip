@@ -18,6 +18,7 @@
 #include "ba3c_band6.h"
 #include "ba3c_conv.h"
 #include "ba3c_problems.h"
+#include "ba3c_rollout.h"
 #include "ba3c_small.h"
 #include "ba3c_split.h"
 #include "ba3c_wgrad.h"
@@ -43,7 +44,6 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kWgradTargetBlocks = 1024;
 constexpr int kMaxBatch = 16384;
-constexpr int kNumCUs = 256;   // MI355X: 8 XCDs x 32 CUs
 
 inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -632,6 +632,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_DBG")) h->dbg = atoi(e);
+
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
   int64_t off = 0;
@@ -900,6 +901,56 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id) {
   h->probe_used = 0;
   h->probe_ms = 0.0;
   h->probe_launches = 0;
+  return BA3C_OK;
+}
+
+int ba3c_nstep_returns(void* stream, const double* reward, const float* value,
+                       const int32_t* start, const int32_t* length, const uint8_t* is_over,
+                       int32_t n_envs, int32_t slots, double gamma, float* R, int32_t* src,
+                       float* init_R, uint8_t* over, int32_t* count) {
+  if (!reward || !value || !start || !length || !is_over || !R || !src || !init_R || !over || !count)
+    return fail(BA3C_ERR_INVALID, "null pointer");
+  if (n_envs < 0 || slots < 1) return fail(BA3C_ERR_INVALID, "bad shape");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  ReturnsArgs a{reward, value, start, length, is_over, n_envs, slots, gamma, R, src, init_R, over, count};
+  hipLaunchKernelGGL(nstep_returns_kernel, dim3(1), dim3(1024), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_gather_rows(void* stream, const void* rows, const int32_t* idx, int32_t n,
+                     int64_t row_bytes, void* out) {
+  if (n < 0) return fail(BA3C_ERR_INVALID, "bad count");
+  if (n == 0) return BA3C_OK;
+  if (!rows || !idx || !out) return fail(BA3C_ERR_INVALID, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (row_bytes == 8) {
+    hipLaunchKernelGGL(gather_i64_kernel, dim3((n + 255) / 256), dim3(256), 0, s,
+                       static_cast<const int64_t*>(rows), idx, n, static_cast<int64_t*>(out));
+  } else if (row_bytes > 0 && row_bytes % 16 == 0 && check_ptr(rows) && check_ptr(out)) {
+    const int words = (int)(row_bytes / 16);
+    const int gx = std::min(8, (words + 255) / 256);
+    hipLaunchKernelGGL(gather_rows16_kernel, dim3(gx, n), dim3(256), 0, s,
+                       static_cast<const uint4*>(rows), idx, n, words, static_cast<uint4*>(out));
+  } else {
+    return fail(BA3C_ERR_INVALID, "row_bytes must be 8 or a multiple of 16 (16-byte aligned rows)");
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_history_push(void* stream, const uint8_t* frame, uint8_t* state, const uint8_t* is_over,
+                      int32_t n_envs, int32_t pixels, int32_t hist_len, int32_t channels) {
+  if (!frame || !state) return fail(BA3C_ERR_INVALID, "null pointer");
+  if (n_envs < 0 || pixels < 1 || hist_len < 1 || channels < 1) return fail(BA3C_ERR_INVALID, "bad shape");
+  if (n_envs == 0) return BA3C_OK;
+  if (hist_len * channels == 4 && channels == 1 && (!check_ptr(state) || (reinterpret_cast<uintptr_t>(frame) & 3)))
+    return fail(BA3C_ERR_INVALID, "state must be 16-byte and frame 4-byte aligned");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HistoryArgs a{frame, state, is_over, n_envs, pixels, hist_len, channels};
+  const int groups = (pixels + 3) / 4;
+  hipLaunchKernelGGL(history_push_kernel, dim3((groups + 255) / 256, n_envs), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
 

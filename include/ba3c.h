@@ -178,6 +178,34 @@ int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
  * fp32 MFMA (v_mfma_f32_*_f32), 0 for a kernel with no matrix work; -1 on a bad id. */
 int ba3c_kernel_split(const ba3c_handle* h, int32_t kernel_id);
 
+/* ---- data formats either side of the path ---------------- */
+
+/* n-step returns of MySimulatorMaster (OpenAIGym/train.py:408-437, _parse_memory) for n_envs
+ * simulators at once.  Env e's memory is a ring of `slots` transitions (i-th oldest at slot
+ * (start[e]+i) % slots), length[e] of them with known rewards (float64, as gym returns them)
+ * and predictor values.  not over: the newest transition only bootstraps (R = its value) and
+ * is not emitted; over: R = 0 and all are emitted.  Emitted in reverse time order, env by env
+ * (the reference's queue order): R = clip(r,-1,1) + gamma*R in float64, stored as float32;
+ * src[i] = e*slots + slot of datapoint i; init_R / over as the reference's datapoint
+ * fields.  Output arrays hold n_envs*slots entries; *count (device int32) receives the
+ * number written.  One workgroup: latency-bound. */
+int ba3c_nstep_returns(void* stream, const double* reward, const float* value,
+                       const int32_t* start, const int32_t* length, const uint8_t* is_over,
+                       int32_t n_envs, int32_t slots, double gamma, float* R, int32_t* src,
+                       float* init_R, uint8_t* over, int32_t* count);
+
+/* BatchData / EnqueueThread hand-off (dataflow/common.py:64-99, train/trainer.py:116-155):
+ * out[i] = rows[idx[i]] for n rows of row_bytes (a multiple of 16, e.g. 84*84*C states, or
+ * exactly 8: int64 actions). */
+int ba3c_gather_rows(void* stream, const void* rows, const int32_t* idx, int32_t n,
+                     int64_t row_bytes, void* out);
+
+/* HistoryFramePlayer (RL/history.py:12-55) for n_envs simulators: state[e] ([pixels][hist_len
+ * * channels] uint8, oldest frame first) becomes concat(state[..., channels:], frame[e]); when
+ * is_over[e] (may be NULL) the frame starts a new episode: zeros + frame. */
+int ba3c_history_push(void* stream, const uint8_t* frame, uint8_t* state, const uint8_t* is_over,
+                      int32_t n_envs, int32_t pixels, int32_t hist_len, int32_t channels);
+
 #ifdef __cplusplus
 }
 #endif

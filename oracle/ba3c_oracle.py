@@ -520,3 +520,67 @@ def init_slots(params, opt="adam", beta1=0.8, beta2=0.75):
     if opt == "adadelta":
         return {"accum": z, "accum_update": {k: np.zeros_like(v) for k, v in params.items()}}
     return {}
+
+
+# --- learner input side: n-step returns (train.py:394-437) and frame history -----------------
+#   Pure-Python restatements, pinned by construction to the
+# reference's own code paths: the same list operations and numpy calls in the same order.
+GAMMA = 0.99                    # train.py:94
+LOCAL_TIME_MAX = 5              # train.py:102
+
+
+def parse_memory(memory, init_r, is_over, gamma=GAMMA):
+    """MySimulatorMaster._parse_memory (train.py:418-437).  memory: list of transitions in
+    time order, each a dict with 'reward' (Python float) and any payload.  Returns the
+    datapoints in queue order as (transition, R, init_r, is_over) with R the float64 value
+    the reference computes (R = np.clip(r, -1, 1) + GAMMA * R over the reversed memory) and
+    the memory left behind ([last] when not over, [] when over)."""
+    mem = list(memory)
+    last = None
+    if not is_over:
+        last = mem[-1]
+        mem = mem[:-1]
+    mem.reverse()
+    R = float(init_r)
+    out = []
+    for k in mem:
+        R = np.clip(k["reward"], -1, 1) + gamma * R
+        out.append((k, R, init_r, is_over))
+    return out, ([last] if not is_over else [])
+
+
+class SimulatorMasterMirror(object):
+    """The per-client memory logic of SimulatorMaster.run (RL/simulator.py:160-185) with
+    MySimulatorMaster's callbacks (train.py:364-437): _on_state appends a transition with the
+    predictor's value and the sampled action; the next message sets its reward and then either
+    _on_episode_over (parse with init_r = 0) or _on_datapoint (parse when LOCAL_TIME_MAX + 1
+    transitions are in memory, bootstrapping from the newest one's value)."""
+
+    def __init__(self, local_time_max=LOCAL_TIME_MAX, gamma=GAMMA):
+        self.T = local_time_max + 1
+        self.gamma = gamma
+        self.memory = {}
+        self.queue = []          # datapoints in put order
+
+    def on_message(self, ident, reward, is_over):
+        mem = self.memory.setdefault(ident, [])
+        if len(mem) > 0:
+            mem[-1]["reward"] = reward
+            if is_over:
+                dps, self.memory[ident] = parse_memory(mem, 0, True, self.gamma)
+                self.queue.extend(dps)
+            elif len(mem) == self.T:
+                dps, self.memory[ident] = parse_memory(mem, mem[-1]["value"], False, self.gamma)
+                self.queue.extend(dps)
+
+    def on_state(self, ident, state_id, action, value):
+        self.memory.setdefault(ident, []).append(
+            {"state": state_id, "action": action, "value": value, "reward": None})
+
+
+def history_state(frames, hist_len):
+    """HistoryFramePlayer.current_state (RL/history.py:29-38): concat of the last hist_len
+    frames along the channel axis, zero frames in front while the history is short."""
+    hist = list(frames)[-hist_len:]
+    pad = [np.zeros_like(hist[0]) for _ in range(hist_len - len(hist))]
+    return np.concatenate(pad + hist, axis=2)

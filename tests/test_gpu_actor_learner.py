@@ -1,0 +1,55 @@
+"""BASELINE configs[0] ("plumbing"): the whole BA3C actor-learner cycle on one GPU with a
+synthetic environment — frame history, predictor forward, numpy-exact sampling, n-step
+returns, BatchData and the fused learner step — runs end to end, and the datapoints the
+learner consumed are the reference simulator master's for the same frames/actions/rewards."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ba3c_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_actor_learner_runs_and_feeds_the_reference_datapoints():
+    from ba3c_amd.actor_learner import ActorLearner
+    from ba3c_amd.model import Model
+    from ba3c_amd.optimizer import AdamOptimizer
+    from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
+    E, B = 24, 32
+    m = Model(num_actions=4, fc_neurons=128, fc_splits=4, batch_size=B, max_batch=max(B, E))
+    m.engine.load_params(O.init_params(128, 4, 4, seed=0, dtype=np.float32))
+    tr = Ba3cTrainer(TrainConfig(model=m, optimizer=AdamOptimizer(1e-3, 0.8, 0.75, 1e-8)))
+    p0 = m.engine.params.clone()
+    loop = ActorLearner(tr, n_envs=E, batch_size=B, seed=1)
+
+    # mirror the simulator master on the host from what the loop's components produce
+    mirror = O.SimulatorMasterMirror()
+    consumed = []
+    orig_put = loop.queue.put
+
+    def put(dps):
+        consumed.extend(zip(dps.action.cpu().numpy().tolist(), dps.R.cpu().numpy().tolist()))
+        orig_put(dps)
+    loop.queue.put = put
+    orig_on_state, orig_on_reward = loop.buf.on_state, loop.buf.on_reward
+
+    def on_state(states, actions, values):
+        for e, (a, v) in enumerate(zip(actions.cpu().numpy(), values.cpu().numpy())):
+            mirror.on_state(e, None, int(a), np.float32(v))
+        orig_on_state(states, actions, values)
+
+    def on_reward(rew, over):
+        for e, (r, o) in enumerate(zip(rew.cpu().numpy(), over.cpu().numpy())):
+            mirror.on_message(e, float(r), bool(o))
+        return orig_on_reward(rew, over)
+    loop.buf.on_state, loop.buf.on_reward = on_state, on_reward
+
+    loop.run(40)
+    torch.cuda.synchronize()
+    assert loop.train_steps >= 4
+    sc = loop.last_scalars.cpu().numpy()
+    assert np.all(np.isfinite(sc))
+    assert not torch.equal(m.engine.params, p0)
+    want = [(k["action"], float(np.float32(R))) for k, R, _, _ in mirror.queue]
+    assert consumed == want and len(want) >= B * loop.train_steps
