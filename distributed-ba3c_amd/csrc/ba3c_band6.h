@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
         const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
         const float v0 = acc[j][0], v1 = acc[j][1], v2 = acc[j][2], v3 = acc[j][3];
         if (w * 4 < G::MROWS && 2 * ph < rows_out) {
-          pos += (v0 > 0.f) + (v1 > 0.f) + (v2 > 0.f) + (v3 > 0.f);
+          pos += count_pos4(v0, v1, v2, v3);   // wave-uniform
           float mx = v0;
           uint32_t arg = 0;
           if (v1 > mx) { mx = v1; arg = 1; }
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
       }
     }
   }
-  if (G::POOL && a.relu_count) relu_count_add(a.relu_count, pos, lane);
+  if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
 
 // fp32 [N][K] band-conv weight copies -> [3][N][K] bf16 splits (hi, mid, lo), one region

@@ -28,6 +28,20 @@ __device__ __forceinline__ void relu_count_add(unsigned long long* slots, unsign
   }
 }
 
+// Wave-uniform variant: count positives with v_cmp -> SGPR mask + s_bcnt1 (scalar ALU), one
+// VALU instruction per value instead of a compare, a select and a 64-bit add.
+__device__ __forceinline__ unsigned long long count_pos4(float v0, float v1, float v2, float v3) {
+  return (unsigned long long)(__popcll(__ballot(v0 > 0.f)) + __popcll(__ballot(v1 > 0.f)) +
+                              __popcll(__ballot(v2 > 0.f)) + __popcll(__ballot(v3 > 0.f)));
+}
+__device__ __forceinline__ void relu_count_add_uniform(unsigned long long* slots, unsigned long long pos,
+                                                       int lane) {
+  if (lane == 0 && pos) {
+    const unsigned slot = (blockIdx.x * 4u + (threadIdx.x >> 6) + blockIdx.y * 977u) & (RELU_SLOTS - 1);
+    atomicAdd(slots + slot, pos);
+  }
+}
+
 // dY at conv-output position (y, x) from pooled grad dP and argmax codes.
 template <int PW, int COUT>
 __device__ __forceinline__ float4 unpool4(const float* __restrict__ dP, const uint8_t* __restrict__ code,

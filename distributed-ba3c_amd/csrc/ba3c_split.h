@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const float v0 = acc[j][nt][0], v1 = acc[j][nt][1], v2 = acc[j][nt][2], v3 = acc[j][nt][3];
-        pos += (v0 > 0.f) + (v1 > 0.f) + (v2 > 0.f) + (v3 > 0.f);
+        pos += count_pos4(v0, v1, v2, v3);   // wave-uniform
         float mx = v0;
         uint32_t arg = 0;
         if (v1 > mx) { mx = v1; arg = 1; }
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
       }
     }
   }
-  if (a.relu_count) relu_count_add(a.relu_count, pos, lane);
+  if (a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
 
 // ---------------------------------------------------------------------------------------
