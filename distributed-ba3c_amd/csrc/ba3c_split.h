@@ -304,20 +304,30 @@ __global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
     for (int i = 0; i < G::NITEM; ++i) {
       const int f = tid + 256 * i, o = f & 31, rest = f >> 5;
       const int pr = rest / (G::PW / 4), q4 = rest - pr * (G::PW / 4);
-      uint32_t hi[4], mid[4], lo[4];
+      // each value split with v_cvt_pk_bf16_f32(v, v): the pair (part, part) lets the
+      // sub-column select be a mask (0x0000FFFF: x even, 0xFFFF0000: x odd)
+      uint32_t part[3][4], mask[4], row[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) split3(yv[i][j], hi[j], mid[j], lo[j]);
+      for (int j = 0; j < 4; ++j) {
+        const float v = yv[i][j];
+        part[0][j] = pack_bf16x2(v, v);
+        const float r1 = v - __uint_as_float(part[0][j] & 0xFFFF0000u);
+        part[1][j] = pack_bf16x2(r1, r1);
+        const float r2 = r1 - __uint_as_float(part[1][j] & 0xFFFF0000u);
+        part[2][j] = pack_bf16x2(r2, r2);
+        const uint32_t k = yc[i][j];                // 0..3, or 255 (no gradient)
+        mask[j] = (k & 1u) ? 0xFFFF0000u : 0x0000FFFFu;
+        row[j] = k >> 1;                            // 0, 1, or 127
+      }
 #pragma unroll
       for (int sy = 0; sy < 2; ++sy) {
         // 8 pixels (pooled j, sub-column sx) of un-pooled row 2 pr + sy
         uint32_t w[3][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint32_t k = yc[i][j];
-          const bool l0 = k == (uint32_t)(2 * sy), l1 = k == (uint32_t)(2 * sy + 1);
-          w[0][j] = (l0 ? hi[j] : 0u) | ((l1 ? hi[j] : 0u) << 16);
-          w[1][j] = (l0 ? mid[j] : 0u) | ((l1 ? mid[j] : 0u) << 16);
-          w[2][j] = (l0 ? lo[j] : 0u) | ((l1 ? lo[j] : 0u) << 16);
+          const bool hit = row[j] == (uint32_t)sy;
+#pragma unroll
+          for (int sp = 0; sp < 3; ++sp) w[sp][j] = hit ? (part[sp][j] & mask[j]) : 0u;
         }
 #pragma unroll
         for (int sp = 0; sp < 3; ++sp)
