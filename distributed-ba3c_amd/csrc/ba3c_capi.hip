@@ -93,7 +93,10 @@ using GConv2D = BandGeom<22, 22, 64, 32, 5, 5, 6, false, 1, 8, 4, 4, 7, 7, 14, 1
 using L6Conv1F = Band6<GConv1F, 192, 32, 7>;
 using L6Conv2F = Band6<GConv2F, 192, 32, 7>;
 using L6Conv1D = Band6<GConv1D, 224, 128, 5>;
-using L6Conv2D = Band6<GConv2D, 224, 128, 4, 32>;   // two 32-channel phases
+// conv2 input gradient: the whole 18x18 map per workgroup in two 32-channel phases (r01r:
+// 0.44 ms at 6-row bands -> 0.31 ms: no halo re-staging, 11 m-blocks per wave hide the
+// weight-fragment latency; 6 and 9-row bands and 8-row conv1 / 12-row conv1-fwd bands measured slower)
+using L6Conv2D = Band6<BandGeom<22, 22, 64, 32, 5, 5, 18, false, 1, 8, 4, 4, 7, 7, 14, 14>, 224, 128, 11, 32>;
 // weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
 using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
 using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
@@ -511,8 +514,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       CHECK(conv_reduce(pl, 2, 32, 32));
     }
     if (h->band) {
-      CHECK(launch_bandx<L6Conv2D>(h, s, BA3C_K_CONV2_DGRAD,
-                                     BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B}, w, WT_C2D));
+      const BandArgs ba{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B};
+      CHECK(launch_bandx<L6Conv2D>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D));
     } else {
       ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
@@ -533,8 +536,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       CHECK(conv_reduce(pl, 1, 32, 32));
     }
     if (h->band) {
-      CHECK(launch_bandx<L6Conv1D>(h, s, BA3C_K_CONV1_DGRAD,
-                                     BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B}, w, WT_C1D));
+      const BandArgs ba{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B};
+      CHECK(launch_bandx<L6Conv1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D));
     } else {
       ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
