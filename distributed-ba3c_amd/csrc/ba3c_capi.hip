@@ -70,8 +70,15 @@ struct ba3c_handle {
   bool band = true;   // band-conv kernels for conv1/conv2 fwd+dgrad (BA3C_GENERIC=1: GEMM engine)
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
-  bool w6 = true;
-  int dbg = 0;        // BA3C_DBG: profiling-only kernel ablations (results are wrong when set)     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  int dbg = 0;        // BA3C_DBG: profiling-only kernel ablations (results are wrong when set)
+  // backward weight gradients on a side stream (BA3C_OVERLAP=1; created on the first training
+  // call that is not being captured). Off by default: r01t/u measured +0.5% step throughput
+  // (561k vs 557k samples/s) because conv1's dgrad and wgrad kernels each fill the chip, and
+  // concurrent kernels make the per-kernel durations (roofline, rocprof) meaningless.
+  bool overlap = false;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -112,7 +119,7 @@ constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64
               WT_TOTAL = WT_C0S + 4 * Conv0S::WB_U4;
 
 struct Workspace {
-  float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *sumsq, *wt;
+  float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *part0, *sumsq, *wt;
   uint16_t* wt6;   // [3][N][K] bf16 splits of the four band-conv weight copies
   uint8_t *c0, *c1, *c2;
   unsigned long long* relu;
@@ -142,18 +149,26 @@ WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN) {
 // geometry constants (train.py:92, :177-212)
 constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
 
+// conv0's weight gradient runs on the main stream while the other weight gradients run on
+// the side stream, so its split-K partials get a region of their own
+size_t max_partials0(const ba3c_handle* h, int B) {
+  size_t mx = 0;
+  const WgradPlan w = plan_wgrad(25 * h->cfg.channels, 32, B * 6400, 128, 32);
+  mx = std::max(mx, (size_t)w.S * w.M * w.N);
+  mx = std::max(mx, (size_t)WG_P0 * GWg0::M * 32);
+  mx = std::max(mx, (size_t)4 * WG_P0S * Conv0W::M * 32);
+  return mx;
+}
+
 size_t max_partials(const ba3c_handle* h, int B) {
-  const int C = h->cfg.channels, F = h->cfg.fc_neurons;
+  const int F = h->cfg.fc_neurons;
   size_t mx = 0;
   auto upd = [&](const WgradPlan& w) { mx = std::max(mx, (size_t)w.S * w.M * w.N); };
-  upd(plan_wgrad(25 * C, 32, B * 6400, 128, 32));
   upd(plan_wgrad(800, 32, B * 1296, 128, 32));
   upd(plan_wgrad(800, 64, B * 196, 128, 64));
   upd(plan_wgrad(576, 64, B * 25, 128, 64));
   upd(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
   upd(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
-  mx = std::max(mx, (size_t)WG_P0 * GWg0::M * 32);
-  mx = std::max(mx, (size_t)4 * WG_P0S * Conv0W::M * 32);
   mx = std::max(mx, (size_t)WG_P1 * GWg1::M * 32);
   mx = std::max(mx, (size_t)WG_P2 * GWg2::M * 64);
   mx = std::max(mx, (size_t)W6_P1 * G6Wg1::M * G6Wg1::COUT);
@@ -193,6 +208,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
     w.dzv = (float*)take(Bz * MAXA * 4);
     w.terms = (float*)take(Bz * NTERMS * 4);
     w.part = (float*)take(max_partials(h, B) * 4);
+    w.part0 = (float*)take(max_partials0(h, B) * 4);
     w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
   } else {
     w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
@@ -435,6 +451,19 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   return BA3C_OK;
 }
 
+// Create the side stream + fork/join events on the first training call made outside a
+// graph capture (stream creation is not a capturable operation).
+int ensure_side_stream(ba3c_handle* h, hipStream_t s) {
+  if (!h->overlap || h->side) return BA3C_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) return BA3C_OK;
+  HIP_TRY(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+  for (auto& e : h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  return BA3C_OK;
+}
+
 template <int CH>
 int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
                  const Workspace& w, float* grads) {
@@ -444,12 +473,26 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   const float* W2c = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3c = prm + h->tensors[h->idx_conv[3]].offset;
   const float* Wfc = prm + h->tensors[h->idx_fc1].offset;
+  // The weight-gradient kernels (heads, fc1, conv3..conv1) run on the side stream `ws`,
+  // each after the event that publishes its output gradient; the input-gradient chain and
+  // conv0's weight gradient (own partials region) stay on `s`, which joins `ws` at the end.
+  hipStream_t ws = s;
+  int nfork = 0;
+  auto fork = [&]() -> int {
+    if (ws == s) return BA3C_OK;
+    HIP_TRY(hipEventRecord(h->ev_fork[nfork], s));
+    HIP_TRY(hipStreamWaitEvent(ws, h->ev_fork[nfork], 0));
+    ++nfork;
+    return BA3C_OK;
+  };
+  if (h->side) ws = h->side;   // joins a graph capture of `s` through the fork events
+  CHECK(fork());
 
   // heads: d fc-pi/W, fc-pi/b, fc-v/W, fc-v/b  (X = h, G = [dz | dV])
   {
     WgradPlan pl = plan_wgrad(F + 1, A + 1, B, 128, 32);
     BatchWgrad g{w.h, w.dzv, w.part, F, MAXA, 1, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_HEAD_WGRAD, g, pl.S)));
+    CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_HEAD_WGRAD, g, pl.S)));
     ReduceMap mp{};
     mp.kind = 2;
     mp.M = pl.M;
@@ -459,13 +502,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.dst_pib = grads + h->tensors[h->idx_pib].offset;
     mp.dst_vW = grads + h->tensors[h->idx_vW].offset;
     mp.dst_vb = grads + h->tensors[h->idx_vb].offset;
-    CHECK(launch_reduce(h, s, w.part, pl.S, mp));
+    CHECK(launch_reduce(h, ws, w.part, pl.S, mp));
   }
   // fc1 weight (+ legacy bias) gradient
   {
     WgradPlan pl = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
     BatchWgrad g{w.a3, w.dh, w.part, 1600, F, legacy ? 1 : 0, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 64, 2, 2>(h, s, BA3C_K_FC1_WGRAD, g, pl.S)));
+    CHECK((launch_gemm<128, 64, 2, 2>(h, ws, BA3C_K_FC1_WGRAD, g, pl.S)));
     ReduceMap mp{};
     mp.kind = 1;
     mp.M = pl.M;
@@ -473,12 +516,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.per = h->per;
     mp.wstride = h->wstride;
     mp.dst = grads + h->tensors[h->idx_fc1].offset;
-    CHECK(launch_reduce(h, s, w.part, pl.S, mp));
+    CHECK(launch_reduce(h, ws, w.part, pl.S, mp));
   }
   // fc1 input gradient -> dY3 (ReluGrad of conv3 fused)
   {
     FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
     CHECK((launch_gemm<128, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
+    CHECK(fork());
   }
   auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad) {
     ReduceMap mp{};
@@ -488,29 +532,30 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.cin = cin;
     mp.cinpad = cinpad;
     mp.dst = grads + h->tensors[h->idx_conv[layer]].offset;
-    return launch_reduce(h, s, w.part, pl.S, mp);
+    return launch_reduce(h, ws, w.part, pl.S, mp);
   };
   // conv3
   {
     WgradPlan pl = plan_wgrad(576, 64, B * 25, 128, 64);
     ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_WGRAD, g, pl.S)));
+    CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
     CHECK(conv_reduce(pl, 3, 64, 64));
     ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0};
     CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
+    CHECK(fork());
   }
   // conv2
   {
     if (h->band && h->w6) {
-      CHECK(launch_wgrad6<G6Wg2>(h, s, BA3C_K_CONV2_WGRAD, Wg6Args{w.p1, w.dp2, w.c2, w.part, B}, W6_P2,
+      CHECK(launch_wgrad6<G6Wg2>(h, ws, BA3C_K_CONV2_WGRAD, Wg6Args{w.p1, w.dp2, w.c2, w.part, B}, W6_P2,
                                  grads + h->tensors[h->idx_conv[2]].offset));
     } else if (h->band) {
-      CHECK(launch_wgband<GWg2>(h, s, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part, B}, WG_P2,
+      CHECK(launch_wgband<GWg2>(h, ws, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part, B}, WG_P2,
                                 grads + h->tensors[h->idx_conv[2]].offset, 32));
     } else {
       WgradPlan pl = plan_wgrad(800, 64, B * 196, 128, 64);
       ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
-      CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_WGRAD, g, pl.S)));
+      CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV2_WGRAD, g, pl.S)));
       CHECK(conv_reduce(pl, 2, 32, 32));
     }
     if (h->band) {
@@ -520,19 +565,20 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
     }
+    CHECK(fork());
   }
   // conv1
   {
     if (h->band && h->w6) {
-      CHECK(launch_wgrad6<G6Wg1>(h, s, BA3C_K_CONV1_WGRAD, Wg6Args{w.p0, w.dp1, w.c1, w.part, B}, W6_P1,
+      CHECK(launch_wgrad6<G6Wg1>(h, ws, BA3C_K_CONV1_WGRAD, Wg6Args{w.p0, w.dp1, w.c1, w.part, B}, W6_P1,
                                  grads + h->tensors[h->idx_conv[1]].offset));
     } else if (h->band) {
-      CHECK(launch_wgband<GWg1>(h, s, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part, B}, WG_P1,
+      CHECK(launch_wgband<GWg1>(h, ws, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part, B}, WG_P1,
                                 grads + h->tensors[h->idx_conv[1]].offset, 32));
     } else {
       WgradPlan pl = plan_wgrad(800, 32, B * 1296, 128, 32);
       ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
-      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_WGRAD, g, pl.S)));
+      CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_CONV1_WGRAD, g, pl.S)));
       CHECK(conv_reduce(pl, 1, 32, 32));
     }
     if (h->band) {
@@ -549,7 +595,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     {
       ProbeScope ps(h, s, BA3C_K_CONV0_WGRAD);
       hipLaunchKernelGGL(conv0s_wgrad_kernel, dim3(P), dim3(256), 0, s,
-                         Conv0WArgs{state, w.dp0, w.c0, w.part, B});
+                         Conv0WArgs{state, w.dp0, w.c0, w.part0, B});
     }
     HIP_TRY(hipGetLastError());
     ReduceMap mp{};
@@ -559,15 +605,26 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.cin = 4;
     mp.cinpad = 16;
     mp.dst = grads + h->tensors[h->idx_conv[0]].offset;
-    CHECK(launch_reduce(h, s, w.part, 4 * P, mp));
+    CHECK(launch_reduce(h, s, w.part0, 4 * P, mp));
   } else if (h->band && CH == 4) {
-    CHECK(launch_wgband<GWg0>(h, s, BA3C_K_CONV0_WGRAD, WgArgs{state, w.dp0, w.c0, w.part, B}, WG_P0,
+    CHECK(launch_wgband<GWg0>(h, s, BA3C_K_CONV0_WGRAD, WgArgs{state, w.dp0, w.c0, w.part0, B}, WG_P0,
                               grads + h->tensors[h->idx_conv[0]].offset, 16));
   } else {
     WgradPlan pl = plan_wgrad(25 * CH, 32, B * 6400, 128, 32);
-    ConvWgrad<true, 84, 84, CH, 5, 5, 32, true> g{state, w.dp0, w.c0, w.part, 1.0f / 255.0f, pl.M, pl.N, pl.K, pl.kchunk};
+    ConvWgrad<true, 84, 84, CH, 5, 5, 32, true> g{state, w.dp0, w.c0, w.part0, 1.0f / 255.0f, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_WGRAD, g, pl.S)));
-    CHECK(conv_reduce(pl, 0, CH, 16));
+    ReduceMap mp{};
+    mp.kind = 0;
+    mp.M = pl.M;
+    mp.N = pl.N;
+    mp.cin = CH;
+    mp.cinpad = 16;
+    mp.dst = grads + h->tensors[h->idx_conv[0]].offset;
+    CHECK(launch_reduce(h, s, w.part0, pl.S, mp));
+  }
+  if (ws != s) {
+    HIP_TRY(hipEventRecord(h->ev_join, ws));
+    HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
   }
   return BA3C_OK;
 }
@@ -635,6 +692,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_DBG")) h->dbg = atoi(e);
+  if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = (e[0] == '1');
 
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
@@ -701,6 +759,10 @@ void ba3c_destroy(ba3c_handle* h) {
   if (!h) return;
   for (auto e : h->ev_begin) (void)hipEventDestroy(e);
   for (auto e : h->ev_end) (void)hipEventDestroy(e);
+  for (auto e : h->ev_fork)
+    if (e) (void)hipEventDestroy(e);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->side) (void)hipStreamDestroy(h->side);
   delete h;
 }
 
@@ -775,6 +837,7 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
     return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  CHECK(ensure_side_stream(h, s));
   Workspace w = carve(h, workspace, batch, true);
   HIP_TRY(hipMemsetAsync(grads, 0, (size_t)h->flat * 4, s));
   HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_SLOTS * 8, s));

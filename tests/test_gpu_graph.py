@@ -53,3 +53,29 @@ def test_captured_step_replays_match_eager_steps():
     assert (b1, b2) == (e1, e2)
     for s_cap, s_eag in zip(cap.optimizer.slots, eager.optimizer.slots):
         np.testing.assert_array_equal(s_cap.cpu().numpy(), s_eag.cpu().numpy())
+
+
+def test_side_stream_weight_gradients_match_single_stream(monkeypatch):
+    """BA3C_OVERLAP=1 runs the backward weight-gradient kernels on a second HIP stream
+    (fork/join events, own split-K partials for conv0): eager and graph-captured steps must
+    equal the single-stream ones bit for bit."""
+    B = 64
+    bs = _batches(B, 4)
+    ref = _trainer(B)
+    for b in [bs[0], bs[0]] + bs[1:]:
+        ref.train_step(*b)
+    monkeypatch.setenv("BA3C_OVERLAP", "1")
+    eager = _trainer(B)
+    for b in [bs[0], bs[0]] + bs[1:]:
+        eager.train_step(*b)
+    cap = _trainer(B)
+    static = tuple(t.clone() for t in bs[0])
+    replay = cap.capture_step(*static, warmup=2)
+    for b in bs[1:]:
+        for dst, src in zip(static, b):
+            dst.copy_(src)
+        replay()
+    torch.cuda.synchronize()
+    want = ref.engine.params.cpu().numpy()
+    np.testing.assert_array_equal(eager.engine.params.cpu().numpy(), want)
+    np.testing.assert_array_equal(cap.engine.params.cpu().numpy(), want)
