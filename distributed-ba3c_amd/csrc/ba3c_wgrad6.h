@@ -47,7 +47,8 @@ struct Wg6Geom {
   static constexpr int XSB = 2 * CW, YSB = 2 * OW;        // bytes per split
   static constexpr int X_BYTES = XROWS * WS * PX, Y_BYTES = KPAD * PY;
   static constexpr int NCG = CIN / CW, NOG = COUT / OW;
-  static constexpr int TAPS0 = (NTAP + 1) / 2;            // taps of wave half 0 (13), half 1: 12
+  static constexpr int TBASE = NTAP / 4, TREM = NTAP % 4;  // taps per wave: 7, 6, 6, 6
+  static constexpr int TW = TBASE + (TREM > 0);
   static constexpr int M = NTAP * CIN;
   static_assert(CW == 16 && OW == 32, "16 input x 32 output channels per workgroup");
   static_assert(PX >= 3 * XSB && PY >= 3 * YSB && PX % 8 == 0 && PY % 8 == 0, "pitches");
@@ -70,17 +71,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cg = blockIdx.y / G::NOG, og = blockIdx.y - cg * G::NOG;
   const int c0 = cg * G::CW, o0 = og * G::OW;
-  const int nb = wave & 1, th = wave >> 1;
-  const int tap0 = th * G::TAPS0;
-  constexpr int T0 = G::TAPS0, T1 = G::NTAP - G::TAPS0;
+  // wave w owns a contiguous run of taps and both 16-column n-blocks, so every X fragment it
+  // reads from LDS feeds two MFMA chains (LDS reads per MFMA 1.08 -> 0.64)
+  const int tap0 = wave * G::TBASE + min(wave, G::TREM);
+  const int ntap = G::TBASE + (wave < G::TREM);
 
   // tr-read lane roles: group g = lane >> 4, row q, column quad p
   const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
   const int kperm = 16 * (g >> 1) + 4 * (g & 1) + q;      // + 8 r for read r
 
-  f32x4 acc[T0];
+  f32x4 acc[G::TW][2];
 #pragma unroll
-  for (int t = 0; t < T0; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < G::TW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // ---- staging work per thread ----
   constexpr int XQ = G::CW / 4;                           // float4 per X pixel (4)
@@ -90,8 +92,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
   constexpr int YN = G::KPAD * YQ;
   constexpr int YPT = (YN + 255) / 256;
   float4 xv[XPT], yv[YPT];
-  uint32_t yc[YPT];
-  int ysub[YPT];
+  uint32_t yc[YPT];                                       // (un-loaded: dY is zero)
 
   const int nbands = a.batch * G::NBANDS;
   auto load_band = [&](int band) {
@@ -115,17 +116,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
       const int ry = p / G::WO, x = p - ry * G::WO;
       yv[i] = f4zero();
       yc[i] = 0;
-      ysub[i] = -1;
       if (f < YN && ry < rows_out) {
         const int y = y0 + ry;
         const size_t pidx = (size_t)(img * G::PH + (y >> 1)) * G::PW + (x >> 1);
         yv[i] = *reinterpret_cast<const float4*>(a.dp + pidx * G::COUT + o0 + oq * 4);
         yc[i] = *reinterpret_cast<const uint32_t*>(a.code + pidx * G::COUT + o0 + oq * 4);
-        ysub[i] = ((y & 1) << 1) | (x & 1);
       }
     }
   };
-  auto store_band = [&]() {
+  auto store_band = [&](int band) {
+    const int y0 = (band - (band / G::NBANDS) * G::NBANDS) * G::RB;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int f = tid + 256 * i;
@@ -145,7 +145,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
       const int f = tid + 256 * i;
       if (f < YN) {
         const int p = f / YQ, oq = f - p * YQ;
-        const uint32_t s = (uint32_t)ysub[i], c = yc[i];
+        const int ry = p / G::WO, x = p - ry * G::WO;
+        const uint32_t s = (((y0 + ry) & 1) << 1) | (x & 1), c = yc[i];
         float e[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == s ? e[k] : 0.f;
@@ -167,7 +168,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
     const int rows_out = min(G::RB, G::HO - (band - img * G::NBANDS) * G::RB);
     const int kvalid = rows_out * G::WO;
     __syncthreads();                                      // previous band's LDS reads done
-    store_band();
+    store_band(band);
     __syncthreads();
     if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
 
@@ -178,21 +179,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         int p = 32 * s + kperm + 8 * r;
-        yb[r] = p * G::PY + nb * 32 + 8 * pq;
+        yb[r] = p * G::PY + 8 * pq;
         if (p >= kvalid) p = 0;                           // padded pixels: dY is zero
         const int y = p / G::WO, x = p - y * G::WO;
         xb[r] = (y * G::WS + x) * G::PX + 8 * pq;
       }
-      bf16x8 b[3];
+      bf16x8 b[2][3];
 #pragma unroll
-      for (int sp = 0; sp < 3; ++sp) {
-        const uint2 u0 = lds_tr16(ys + yb[0] + sp * G::YSB);
-        const uint2 u1 = lds_tr16(ys + yb[1] + sp * G::YSB);
-        b[sp] = as_bf16x8(u0, u1);
-      }
+      for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-      for (int t = 0; t < T0; ++t) {
-        if (th == 1 && t >= T1) break;
+        for (int sp = 0; sp < 3; ++sp) {
+          const uint2 u0 = lds_tr16(ys + yb[0] + nb * 32 + sp * G::YSB);
+          const uint2 u1 = lds_tr16(ys + yb[1] + nb * 32 + sp * G::YSB);
+          b[nb][sp] = as_bf16x8(u0, u1);
+        }
+#pragma unroll
+      for (int t = 0; t < G::TW; ++t) {
+        if (t >= ntap) break;
         const int tap = tap0 + t;
         const int kh = tap / G::KW, kw = tap - kh * G::KW;
         const int toff = (kh * G::WS + kw) * G::PX;
@@ -203,27 +206,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
           const uint2 u1 = lds_tr16(xs + xb[1] + toff + sp * G::XSB);
           av[sp] = as_bf16x8(u0, u1);
         }
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[0], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[1], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[0], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[2], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[1], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], b[0], acc[t], 0, 0, 0);
+        // a1b1, a1b2, a2b1, a1b3, a2b2, a3b1 — interleaved over the two n-blocks
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[nb][0], acc[t][nb], 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[nb][1], acc[t][nb], 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[nb][0], acc[t][nb], 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[nb][2], acc[t][nb], 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[nb][1], acc[t][nb], 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], b[nb][0], acc[t][nb], 0, 0, 0);
       }
     }
   }
 
   // ---- epilogue: C layout 16x16: lane holds column (lane & 15) = o, rows 4*(lane>>4)+r = c ----
   float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
-  const int o = o0 + nb * 16 + (lane & 15);
 #pragma unroll
-  for (int t = 0; t < T0; ++t) {
-    if (th == 1 && t >= T1) break;
+  for (int t = 0; t < G::TW; ++t) {
+    if (t >= ntap) break;
     const int tap = tap0 + t;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = c0 + 4 * (lane >> 4) + r;
-      pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[t][r];
+    for (int nb = 0; nb < 2; ++nb) {
+      const int o = o0 + nb * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + 4 * (lane >> 4) + r;
+        pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[t][nb][r];
+      }
     }
   }
 }
