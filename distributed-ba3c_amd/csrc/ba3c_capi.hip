@@ -112,7 +112,7 @@ constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
 using G6Wg1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 224>;
 using G6Wg2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 192>;
 constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workgroups
-constexpr int WG_P0S = 256;   // conv0s_wgrad_kernel: one 141 KB-LDS workgroup per CU
+constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
               WT_C2D = WT_C1D + 800 * 32, WT_C0F = WT_C2D + 1600 * 32,
               WT_C0S = WT_C0F + 32 * Conv0Geom::KDIM,            // uint4 [Conv0S::WB_U4]
@@ -156,7 +156,7 @@ size_t max_partials0(const ba3c_handle* h, int B) {
   const WgradPlan w = plan_wgrad(25 * h->cfg.channels, 32, B * 6400, 128, 32);
   mx = std::max(mx, (size_t)w.S * w.M * w.N);
   mx = std::max(mx, (size_t)WG_P0 * GWg0::M * 32);
-  mx = std::max(mx, (size_t)4 * WG_P0S * Conv0W::M * 32);
+  mx = std::max(mx, (size_t)WG_P0S * Conv0W::M * 32);
   return mx;
 }
 
@@ -605,7 +605,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.cin = 4;
     mp.cinpad = 16;
     mp.dst = grads + h->tensors[h->idx_conv[0]].offset;
-    CHECK(launch_reduce(h, s, w.part0, 4 * P, mp));
+    CHECK(launch_reduce(h, s, w.part0, P, mp));
   } else if (h->band && CH == 4) {
     CHECK(launch_wgband<GWg0>(h, s, BA3C_K_CONV0_WGRAD, WgArgs{state, w.dp0, w.c0, w.part0, B}, WG_P0,
                               grads + h->tensors[h->idx_conv[0]].offset, 16));

@@ -234,54 +234,62 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
 //   X: two copies of the RB + 4 input rows, channel-planar bf16, copy h shifted left by h
 //      pixels, so the 8 pixels a lane feeds for tap (kh, kw) start at an even column of copy
 //      kw & 1 (dword aligned);
-//   Y: [split][o][pixel] bf16, o pitch 648 pixels (324 dwords = 4 banks apart: the 16 lanes
-//      of a ds_read_b128 group hit 16 distinct bank quads).
+//   Y: the POOLED gradient dP of the band, split: [split][pooled row][o][pooled col] bf16,
+//      plus its argmax codes [pooled row][o][pooled col] u8 — a quarter of the un-pooled
+//      dY's bytes, so staging writes 4x less and three workgroups fit a CU.  The MFMA B
+//      fragment (8 un-pooled pixels = 4 windows x 2 sub-columns of one row) is un-pooled in
+//      registers: window j's dword is (v, v) & mask, mask = 0x0000FFFF / 0xFFFF0000 for the
+//      argmax sub-column, 0 when the argmax is in the other row or there is no gradient.
+//      o pitch 40 bf16 = 20 dwords: the 16 o of a lane group land on 16 distinct bank pairs.
 // K-step s of a band = pixels 32s .. 32s + 31 (row-major over the band), lane group q
 // supplies pixels 32s + 8q .. + 7 (one row, since 80 % 8 == 0); waves take K-steps
 // s = wave, wave + 4, ...  The next band's global loads are issued into registers before
-// the MFMA phase of the current one.  Each wave writes one partial slab (scaled by 1/255).
+// the MFMA phase of the current one.  Each workgroup writes one partial slab (x 1/255).
 // ---------------------------------------------------------------------------------------
 struct Conv0W {
   static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
   static constexpr int HO = 80, WO = 80, PH = 40, PW = 40;
   static constexpr int RB = 8, NBANDS = HO / RB, XROWS = RB + KT - 1;   // 12 rows (<= 84)
+  static constexpr int PRB = RB / 2;               // pooled rows per band (4)
   static constexpr int KPB = RB * WO;              // 640 pixels per band
   static constexpr int KSTEPS = KPB / 32;          // 20
   static constexpr int KSW = KSTEPS / 4;           // 5 per wave
-  static constexpr int YP = 648;                   // o pitch (bf16)
-  static constexpr int Y_BF16 = 3 * COUT * YP;
+  static constexpr int Y_BF16 = 3 * PRB * COUT * PW;                  // 15360
+  static constexpr int YC_BYTES = PRB * COUT * PW;                    // 5120
   static constexpr int XP = 88;                    // row pitch (bf16)
   static constexpr int XPL = XROWS * XP;           // channel plane
   static constexpr int XCP = C * XPL;              // copy
   static constexpr int X_BF16 = 2 * XCP;
-  static constexpr int LDS_U4 = (Y_BF16 + X_BF16) * 2 / 16;
+  static constexpr int LDS_U4 = ((Y_BF16 + X_BF16) * 2 + YC_BYTES) / 16;
   static constexpr int MT = 7, M = NTAP * C;
-  static constexpr int NITEM = COUT * (RB / 2) * (PW / 4) / 256;       // dY items per thread
+  static constexpr int NITEM = COUT * PRB * (PW / 4) / 256;            // dP items per thread
   static constexpr int NXV = XROWS * WS * C / 16;                      // uint4 of frame rows
-  static_assert(KSTEPS % 4 == 0 && COUT * (RB / 2) * (PW / 4) % 256 == 0 && NXV <= 256, "geom");
+  static_assert(KSTEPS % 4 == 0 && COUT * PRB * (PW / 4) % 256 == 0 && NXV <= 256, "geom");
   static_assert(HO % RB == 0 && RB + KT - 1 + HO - RB <= HS, "band rows stay inside the frame");
+  static_assert(WO % 8 == 0 && ((Y_BF16 + X_BF16) * 2) % 16 == 0, "layout");
 };
 
 struct Conv0WArgs {
   const uint8_t* x;        // frames [B,84,84,4]
   const float* dp;         // dP0 [B,40,40,32]
   const uint8_t* code;     // argmax codes of dP0
-  float* part;             // [4 * gridDim.x][100][32] partial slabs
+  float* part;             // [gridDim.x][100][32] partial slabs
   int batch;
 };
 
-__global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv0s_wgrad_kernel(const Conv0WArgs a) {
   using G = Conv0W;
   __shared__ uint4 lds[G::LDS_U4];
   uint16_t* ys = reinterpret_cast<uint16_t*>(lds);
   uint16_t* xs = ys + G::Y_BF16;
+  uint8_t* yc8 = reinterpret_cast<uint8_t*>(xs + G::X_BF16);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int nbands = a.batch * G::NBANDS;
 
   // ---- per-thread prefetch registers for one band ----
   float yv[G::NITEM][4];
-  uint32_t yc[G::NITEM][4];
+  uint32_t yc[G::NITEM];
   uint4 xv;
   auto load_band = [&](int band) {
     const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
@@ -290,11 +298,13 @@ __global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
       const int f = tid + 256 * i, o = f & 31, rest = f >> 5;
       const int pr = rest / (G::PW / 4), q4 = rest - pr * (G::PW / 4);
       const size_t base = ((size_t)(img * G::PH + y0 / 2 + pr) * G::PW + 4 * q4) * G::COUT + o;
+      uint32_t c = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         yv[i][j] = a.dp[base + j * G::COUT];
-        yc[i][j] = a.code[base + j * G::COUT];
+        c |= (uint32_t)a.code[base + j * G::COUT] << (8 * j);
       }
+      yc[i] = c;
     }
     xv = tid < G::NXV ? reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C)[tid]
                       : make_uint4(0, 0, 0, 0);
@@ -304,36 +314,15 @@ __global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
     for (int i = 0; i < G::NITEM; ++i) {
       const int f = tid + 256 * i, o = f & 31, rest = f >> 5;
       const int pr = rest / (G::PW / 4), q4 = rest - pr * (G::PW / 4);
-      // each value split with v_cvt_pk_bf16_f32(v, v): the pair (part, part) lets the
-      // sub-column select be a mask (0x0000FFFF: x even, 0xFFFF0000: x odd)
-      uint32_t part[3][4], mask[4], row[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = yv[i][j];
-        part[0][j] = pack_bf16x2(v, v);
-        const float r1 = v - __uint_as_float(part[0][j] & 0xFFFF0000u);
-        part[1][j] = pack_bf16x2(r1, r1);
-        const float r2 = r1 - __uint_as_float(part[1][j] & 0xFFFF0000u);
-        part[2][j] = pack_bf16x2(r2, r2);
-        const uint32_t k = yc[i][j];                // 0..3, or 255 (no gradient)
-        mask[j] = (k & 1u) ? 0xFFFF0000u : 0x0000FFFFu;
-        row[j] = k >> 1;                            // 0, 1, or 127
-      }
-#pragma unroll
-      for (int sy = 0; sy < 2; ++sy) {
-        // 8 pixels (pooled j, sub-column sx) of un-pooled row 2 pr + sy
-        uint32_t w[3][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool hit = row[j] == (uint32_t)sy;
-#pragma unroll
-          for (int sp = 0; sp < 3; ++sp) w[sp][j] = hit ? (part[sp][j] & mask[j]) : 0u;
-        }
-#pragma unroll
-        for (int sp = 0; sp < 3; ++sp)
-          *reinterpret_cast<uint4*>(ys + (sp * G::COUT + o) * G::YP + (2 * pr + sy) * G::WO + 8 * q4) =
-              make_uint4(w[sp][0], w[sp][1], w[sp][2], w[sp][3]);
-      }
+      uint32_t h0, m0, l0, h1, m1, l1;
+      split3x2(yv[i][0], yv[i][1], h0, m0, l0);
+      split3x2(yv[i][2], yv[i][3], h1, m1, l1);
+      const int e = (pr * G::COUT + o) * G::PW + 4 * q4;
+      constexpr int SP = G::PRB * G::COUT * G::PW;
+      *reinterpret_cast<uint2*>(ys + e) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(ys + SP + e) = make_uint2(m0, m1);
+      *reinterpret_cast<uint2*>(ys + 2 * SP + e) = make_uint2(l0, l1);
+      *reinterpret_cast<uint32_t*>(yc8 + e) = yc[i];
     }
     if (tid < G::NXV) {
       const int p = 4 * tid, r = p / G::WS, x = p - r * G::WS;    // 4 pixels of one row
@@ -362,7 +351,6 @@ __global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
     const int c = li & 3, kh = tap / G::KT, kw = tap % G::KT, h = kw & 1;
     aoff[mt] = h * G::XCP + c * G::XPL + kh * G::XP + (kw - h);
   }
-  const int yoff = li * G::YP + 8 * lq;                 // + (sp * 32 + 16 nt) * YP + 32 s
 
   f32x4 acc[G::MT][2];
 #pragma unroll
@@ -387,14 +375,31 @@ __global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
         const u32x4 u = {p[0], p[1], p[2], p[3]};
         av[mt] = __builtin_bit_cast(bf16x8, u);
       }
+      // B: un-pool 4 windows (pooled cols x0/2 .. +3 of pooled row r/2) for channel o
+      const uint32_t sy = (uint32_t)(r & 1);
+      const int e0 = ((r >> 1) * G::COUT + li) * G::PW + (x0 >> 1);
       bf16x8 bv[3][2];
 #pragma unroll
-      for (int sp = 0; sp < 3; ++sp)
+      for (int nt = 0; nt < 2; ++nt) {
+        const int e = e0 + 16 * nt * G::PW;
+        const uint32_t cw = *reinterpret_cast<const uint32_t*>(yc8 + e);
+        uint32_t mk[4];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const uint4 u = *reinterpret_cast<const uint4*>(ys + (sp * G::COUT + 16 * nt) * G::YP + yoff + 32 * s);
-          bv[sp][nt] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t k = (cw >> (8 * j)) & 255u;   // 0..3, or 255 (no gradient)
+          mk[j] = (k >> 1) == sy ? ((k & 1u) ? 0xFFFF0000u : 0x0000FFFFu) : 0u;
         }
+#pragma unroll
+        for (int sp = 0; sp < 3; ++sp) {
+          const uint2 u = *reinterpret_cast<const uint2*>(ys + sp * (G::PRB * G::COUT * G::PW) + e);
+          // (lo, lo) and (hi, hi) half-word pairs of each dword
+          const u32x4 w = {__builtin_amdgcn_perm(u.x, u.x, 0x01000100u) & mk[0],
+                           __builtin_amdgcn_perm(u.x, u.x, 0x03020302u) & mk[1],
+                           __builtin_amdgcn_perm(u.y, u.y, 0x01000100u) & mk[2],
+                           __builtin_amdgcn_perm(u.y, u.y, 0x03020302u) & mk[3]};
+          bv[sp][nt] = __builtin_bit_cast(bf16x8, w);
+        }
+      }
 #pragma unroll
       for (int sp = 0; sp < 3; ++sp)
 #pragma unroll
@@ -405,9 +410,11 @@ __global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
     }
   }
 
-  // ---- epilogue: slab (block, wave); lane holds rows 16 mt + 4 lq + r, column 16 nt + li ----
-  float* pz = a.part + ((size_t)blockIdx.x * 4 + wave) * G::M * G::COUT;
-  const float inv255 = 1.0f / 255.0f;
+  // ---- epilogue: the four waves' accumulators go through LDS and are summed in wave order
+  // into ONE slab per workgroup (lane holds rows 16 mt + 4 lq + r, column 16 nt + li) ----
+  static_assert(4 * G::M * G::COUT * 4 <= G::LDS_U4 * 16, "slab staging fits the band LDS");
+  float* red = reinterpret_cast<float*>(lds);
+  __syncthreads();                                     // last band's LDS reads are done
 #pragma unroll
   for (int mt = 0; mt < G::MT; ++mt)
 #pragma unroll
@@ -415,8 +422,15 @@ __global__ void __launch_bounds__(256) conv0s_wgrad_kernel(const Conv0WArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * mt + 4 * lq + r;
-        if (m < G::M) pz[(size_t)m * G::COUT + 16 * nt + li] = acc[mt][nt][r] * inv255;
+        if (m < G::M) red[(wave * G::M + m) * G::COUT + 16 * nt + li] = acc[mt][nt][r];
       }
+  __syncthreads();
+  float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
+  const float inv255 = 1.0f / 255.0f;
+  for (int e = tid; e < G::M * G::COUT; e += 256) {
+    constexpr int W = G::M * G::COUT;
+    pz[e] = (((red[e] + red[W + e]) + red[2 * W + e]) + red[3 * W + e]) * inv255;
+  }
 }
 
 }  // namespace ba3c
