@@ -112,6 +112,7 @@ constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
 using G6Wg1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 224>;
 using G6Wg2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 192>;
 constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workgroups
+constexpr int FW_P0S = 512;   // conv0s_fwd_kernel: persistent, two workgroups per CU
 constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
               WT_C2D = WT_C1D + 800 * 32, WT_C0F = WT_C2D + 1600 * 32,
@@ -381,7 +382,7 @@ int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a) {
                         reinterpret_cast<const uint4*>(a.wt - WT_C0F + WT_C0S), a.out, a.out_code,
                         a.relu_count, a.batch};
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-    hipLaunchKernelGGL(conv0s_fwd_kernel, dim3(a.batch * Conv0S::NBANDS), dim3(256), 0, s, sa);
+    hipLaunchKernelGGL(conv0s_fwd_kernel, dim3(std::min(FW_P0S, a.batch * Conv0S::NBANDS)), dim3(256), 0, s, sa);
   } else {
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
     hipLaunchKernelGGL(conv0_band_kernel, dim3(a.batch * Conv0Geom::NBANDS), dim3(256), 0, s, a);

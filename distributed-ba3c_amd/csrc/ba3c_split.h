@@ -101,9 +101,12 @@ __global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restri
                    part[sp][4] | (part[sp][5] << 16), part[sp][6] | (part[sp][7] << 16));
 }
 
-// One workgroup = one image x one band of RB output rows (RB/2 pooled rows); wave w owns
-// pooled rows 2w, 2w+1 of the band = 20 m-blocks of 4 windows, both 16-channel n-tiles.
-// M rows are ordered (window, sub) so a lane's 4 accumulator rows are one 2x2 window.
+// Persistent workgroups walk bands (one image x RB output rows = RB/2 pooled rows); wave w
+// owns pooled rows 2w, 2w+1 of a band = 20 m-blocks of 4 windows, both 16-channel n-tiles.
+// The weight splits are loaded into registers once per workgroup, and the next band's frame
+// rows are loaded into registers before the current band's MFMAs, so HBM latency hides
+// behind the arithmetic.  M rows are ordered (window, sub) so a lane's 4 accumulator rows
+// are one 2x2 window.
 struct Conv0SArgs {
   const uint8_t* x;        // frames [B,84,84,4]
   const uint4* wb;         // prepared bf16 weight splits
@@ -117,39 +120,41 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
   using G = Conv0S;
   __shared__ uint2 xs[G::SROWS * G::WS];            // bf16 pixels (4 channels), 13.4 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int img = blockIdx.x / G::NBANDS;
-  const int y0 = (blockIdx.x - img * G::NBANDS) * G::RB;
+  const int nbands = a.batch * G::NBANDS;
 
-  // ---- stage rows [y0, y0 + SROWS): contiguous 16-byte loads (4 pixels), all in flight ----
-  {
-    constexpr int NV = G::SROWS * G::WS / 4;       // 420 uint4
-    constexpr int NPT = (NV + 255) / 256;
+  // ---- rows [y0, y0 + SROWS) of a band: contiguous 16-byte loads (4 pixels) ----
+  constexpr int NV = G::SROWS * G::WS / 4;         // 420 uint4
+  constexpr int NPT = (NV + 255) / 256;
+  uint4 v[NPT];
+  auto load_band = [&](int band) {
+    const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
     const uint4* src = reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
-    uint4 v[NPT];
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int f = tid + 256 * i;
       v[i] = f < NV ? src[f] : make_uint4(0, 0, 0, 0);
     }
+  };
+  auto store_band = [&]() {
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int f = tid + 256 * i;
       if (f < NV) {
         const uint32_t px[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-        uint4 lo, hi;
         uint32_t o[8];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           o[2 * p] = u8_bf16(px[p] & 255u) | (u8_bf16((px[p] >> 8) & 255u) << 16);
           o[2 * p + 1] = u8_bf16((px[p] >> 16) & 255u) | (u8_bf16(px[p] >> 24) << 16);
         }
-        lo = make_uint4(o[0], o[1], o[2], o[3]);
-        hi = make_uint4(o[4], o[5], o[6], o[7]);
-        reinterpret_cast<uint4*>(xs)[2 * f] = lo;
-        reinterpret_cast<uint4*>(xs)[2 * f + 1] = hi;
+        reinterpret_cast<uint4*>(xs)[2 * f] = make_uint4(o[0], o[1], o[2], o[3]);
+        reinterpret_cast<uint4*>(xs)[2 * f + 1] = make_uint4(o[4], o[5], o[6], o[7]);
       }
     }
-  }
+  };
+
+  int band = blockIdx.x;
+  if (band < nbands) load_band(band);
 
   const int li = lane & 15, lq = lane >> 4;
   bf16x8 wf[G::NSPLIT][2][G::KSTEPS];
@@ -173,50 +178,56 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
       const int tap = 8 * s + 2 * lq + h;
       lb[s][h] = pix0 + (tap < G::NTAP ? (tap / G::KT) * G::WS + tap % G::KT : 0);
     }
-  __syncthreads();
 
   unsigned long long pos = 0;
   const float inv255 = 1.0f / 255.0f;
+  for (; band < nbands; band += gridDim.x) {
+    const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
+    __syncthreads();                                 // previous band's LDS reads are done
+    store_band();
+    __syncthreads();
+    if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
 #pragma unroll
-  for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
-    f32x4 acc[G::MCH][2];
+    for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
+      f32x4 acc[G::MCH][2];
 #pragma unroll
-    for (int j = 0; j < G::MCH; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < G::MCH; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < G::KSTEPS; ++s) {
-      bf16x8 af[G::MCH];
+      for (int s = 0; s < G::KSTEPS; ++s) {
+        bf16x8 af[G::MCH];
+#pragma unroll
+        for (int j = 0; j < G::MCH; ++j) {
+          const int jj = ch * G::MCH + j;
+          const int off = (jj / G::MBROW) * 2 * G::WS + (jj % G::MBROW) * 8;   // immediate
+          af[j] = as_bf16x8(xs[lb[s][0] + off], xs[lb[s][1] + off]);
+        }
+#pragma unroll
+        for (int sp = 0; sp < G::NSPLIT; ++sp)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int j = 0; j < G::MCH; ++j)
+              acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], wf[sp][nt][s], acc[j][nt], 0, 0, 0);
+      }
+      // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nt*16 + li
 #pragma unroll
       for (int j = 0; j < G::MCH; ++j) {
         const int jj = ch * G::MCH + j;
-        const int off = (jj / G::MBROW) * 2 * G::WS + (jj % G::MBROW) * 8;   // immediate
-        af[j] = as_bf16x8(xs[lb[s][0] + off], xs[lb[s][1] + off]);
-      }
+        const int ph = y0 / 2 + 2 * wave + jj / G::MBROW;
+        const int pw = 4 * (jj % G::MBROW) + lq;
 #pragma unroll
-      for (int sp = 0; sp < G::NSPLIT; ++sp)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-          for (int j = 0; j < G::MCH; ++j)
-            acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], wf[sp][nt][s], acc[j][nt], 0, 0, 0);
-    }
-    // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nt*16 + li
-#pragma unroll
-    for (int j = 0; j < G::MCH; ++j) {
-      const int jj = ch * G::MCH + j;
-      const int ph = y0 / 2 + 2 * wave + jj / G::MBROW;
-      const int pw = 4 * (jj % G::MBROW) + lq;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const float v0 = acc[j][nt][0], v1 = acc[j][nt][1], v2 = acc[j][nt][2], v3 = acc[j][nt][3];
-        pos += count_pos4(v0, v1, v2, v3);   // wave-uniform
-        float mx = v0;
-        uint32_t arg = 0;
-        if (v1 > mx) { mx = v1; arg = 1; }
-        if (v2 > mx) { mx = v2; arg = 2; }
-        if (v3 > mx) { mx = v3; arg = 3; }
-        const size_t o = ((size_t)(img * (G::HO / 2) + ph) * (G::WO / 2) + pw) * G::COUT + nt * 16 + li;
-        a.out[o] = mx > 0.f ? mx * inv255 : 0.f;
-        if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+        for (int nt = 0; nt < 2; ++nt) {
+          const float v0 = acc[j][nt][0], v1 = acc[j][nt][1], v2 = acc[j][nt][2], v3 = acc[j][nt][3];
+          pos += count_pos4(v0, v1, v2, v3);   // wave-uniform
+          float mx = v0;
+          uint32_t arg = 0;
+          if (v1 > mx) { mx = v1; arg = 1; }
+          if (v2 > mx) { mx = v2; arg = 2; }
+          if (v3 > mx) { mx = v3; arg = 3; }
+          const size_t o = ((size_t)(img * (G::HO / 2) + ph) * (G::WO / 2) + pw) * G::COUT + nt * 16 + li;
+          a.out[o] = mx > 0.f ? mx * inv255 : 0.f;
+          if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+        }
       }
     }
   }
