@@ -120,7 +120,7 @@ constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64
               WT_TOTAL = WT_C0S + 4 * Conv0S::WB_U4;
 
 struct Workspace {
-  float *p0, *p1, *p2, *a3, *h, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *part0, *sumsq, *wt;
+  float *p0, *p1, *p2, *a3, *h, *fcpart, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *part0, *sumsq, *wt;
   uint16_t* wt6;   // [3][N][K] bf16 splits of the four band-conv weight copies
   uint8_t *c0, *c1, *c2;
   unsigned long long* relu;
@@ -149,6 +149,8 @@ WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN) {
 
 // geometry constants (train.py:92, :177-212)
 constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
+constexpr int FC_KCHUNK = 416, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;   // FC1 fwd split-K
+static_assert(FC_KCHUNK % GEMM_BK == 0, "k-chunk of whole k-tiles");
 
 // conv0's weight gradient runs on the main stream while the other weight gradients run on
 // the side stream, so its split-K partials get a region of their own
@@ -194,6 +196,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   w.p2 = (float*)take(Bz * P2 * 4);
   w.a3 = (float*)take(Bz * A3 * 4);
   w.h = (float*)take(Bz * F * 4);
+  w.fcpart = (float*)take((size_t)FC_SPLIT * Bz * F * 4);
   w.relu = (unsigned long long*)take(RELU_SLOTS * 8);
   w.wt = (float*)take((size_t)WT_TOTAL * 4);
   w.wt6 = (uint16_t*)take((size_t)3 * WT_C0F * 2);
@@ -446,9 +449,18 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   }
   ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
   CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
+  // split-K: K = 1600 in FC_SPLIT fixed chunks (a 128x64 tile over all of K is one
+  // workgroup's 50 serial k-tiles: latency-bound at any batch), then one finishing pass
   FcFwd fc{w.a3, prm + h->tensors[h->idx_fc1].offset, w.h, rc, h->per, h->wstride,
-           h->cfg.replace_with_conv ? 0 : 1, B, F, 1600, 0};
-  CHECK((launch_gemm<128, 64, 2, 2>(h, s, BA3C_K_FC1_FWD, fc, 1)));
+           h->cfg.replace_with_conv ? 0 : 1, B, F, 1600, FC_KCHUNK, w.fcpart};
+  {
+    ProbeScope ps(h, s, BA3C_K_FC1_FWD);
+    hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, FcFwd>), dim3((B + 127) / 128, (F + 63) / 64, FC_SPLIT),
+                       dim3(GEMM_THREADS), 0, s, fc);
+    const int nblk = (int)std::min<size_t>(((size_t)B * F + 255) / 256, 2048);
+    hipLaunchKernelGGL(fc_finish_kernel, dim3(nblk), dim3(256), 0, s, fc, FC_SPLIT);
+  }
+  HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
 

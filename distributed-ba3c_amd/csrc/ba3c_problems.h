@@ -301,6 +301,8 @@ struct FcFwd {
   unsigned long long* relu_count;
   int per, wstride, legacy;
   int M, N, K, kchunk;
+  float* part;          // split-K (kchunk > 0): raw partial slabs [z][M][N]; fc_finish_kernel
+                        // sums them in z order and applies the epilogue below
 
   __device__ int a_row(int m) const { return m < M ? m * 1600 : -1; }
   __device__ float4 a_load(int row, int k, int kend) const {
@@ -317,8 +319,23 @@ struct FcFwd {
     return *reinterpret_cast<const float4*>(w1 + c + (size_t)k * per);
   }
   template <int TM, int TN>
-  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
+  __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int z) const {
     const int j = lane & 31;
+    if (part) {
+      float* pz = part + (size_t)z * M * N;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int col = ncol + b * 32 + j;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = mrow + a * 32 + acc_row(r, lane);
+            if (m < M && col < N) pz[(size_t)m * N + col] = acc[a][b][r];
+          }
+        }
+      return;
+    }
     unsigned long long pos = 0;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -344,6 +361,26 @@ struct FcFwd {
     if (legacy && relu_count) relu_count_add(relu_count, pos, lane);
   }
 };
+
+// FC1 forward, split-K finish: h[m][n] = epilogue(sum_z part[z][m][n]) with FcFwd's
+// epilogue (legacy: + bias, ReLU, positive count).  The split is fixed (FC_SPLIT chunks of
+// FC_KCHUNK), so every row's summation order — and so its rounding — is the same at any batch.
+__global__ void __launch_bounds__(256) fc_finish_kernel(const FcFwd p, int S) {
+  const int lane = threadIdx.x & 63;
+  const size_t MN = (size_t)p.M * p.N;
+  unsigned long long pos = 0;
+  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < MN; e += (size_t)gridDim.x * 256) {
+    float v = p.part[e];
+    for (int z = 1; z < S; ++z) v += p.part[(size_t)z * MN + e];
+    if (p.legacy) {
+      const int col = (int)(e % p.N), sidx = col / p.per;
+      v = fmaxf(v + p.w1[sidx * p.wstride + 1600 * p.per + (col - sidx * p.per)], 0.f);
+      pos += v > 0.f;
+    }
+    p.h[e] = v;
+  }
+  if (p.legacy && p.relu_count) relu_count_add(p.relu_count, pos, lane);
+}
 
 // FC1 input gradient: dY3[b][j] = (sum_f dh[b][f] W1[j][f]) * (a3[b][j] > 0)
 struct FcDgrad {
