@@ -448,7 +448,7 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
     CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
   }
   ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
-  CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
+  CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
   // split-K: K = 1600 in FC_SPLIT fixed chunks (a 128x64 tile over all of K is one
   // workgroup's 50 serial k-tiles: latency-bound at any batch), then one finishing pass
   FcFwd fc{w.a3, prm + h->tensors[h->idx_fc1].offset, w.h, rc, h->per, h->wstride,
@@ -534,7 +534,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // fc1 input gradient -> dY3 (ReluGrad of conv3 fused)
   {
     FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
-    CHECK((launch_gemm<128, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
+    CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
     CHECK(fork());
   }
   auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad) {
@@ -554,7 +554,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
     CHECK(conv_reduce(pl, 3, 64, 64));
     ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0};
-    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
+    CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
     CHECK(fork());
   }
   // conv2
