@@ -11,6 +11,7 @@ constexpr int MAXA = 32;        // dz|dv row pitch; num_actions <= 31
 constexpr int NTERMS = 8;       // per-sample loss terms
 constexpr int MAXT = 48;        // max tensors in the flat layout
 constexpr int UPD_CHUNK = 4096; // floats per workgroup in clip / update kernels
+static_assert(UPD_CHUNK % 256 == 0, "whole elements per thread");
 
 // ---------------------------------------------------------------------------------------
 // Heads: one wave per sample.  z = h W_pi + b_pi, V = h W_v + b_v, p = softmax(z),
@@ -325,9 +326,13 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g,
 }
 
 // clip_by_average_norm multiplier of tensor t: min(rsqrt(sum g^2) * n, 1/0.1)
+// Sum of the tensor's per-chunk partials: lane-strided, then a butterfly over the wave (every
+// lane ends with the same, order-fixed value) — a serial loop over up to ~200 partials was a
+// chain of dependent L2 round trips in every update workgroup.
 __device__ __forceinline__ float clip_factor(const TensorTable& tt, int t, const float* part) {
   float ss = 0.f;
-  for (int b = tt.chunk0[t]; b < tt.chunk0[t + 1]; ++b) ss += part[b];
+  for (int b = tt.chunk0[t] + (int)(threadIdx.x & 63); b < tt.chunk0[t + 1]; b += 64) ss += part[b];
+  ss = wave_sum_f(ss);
   return fminf(rsqrtf(ss) * (float)tt.numel[t], 10.0f);
 }
 
@@ -379,13 +384,34 @@ __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const T
   const float f = a.clip_part ? clip_factor(tt, t, a.clip_part) : 0.f;
   const float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1])
                                                  : a.alpha;
-  for (int i = beg + threadIdx.x; i < end; i += 256) {
+  // all loads of the thread's UPD_CHUNK / 256 elements are issued before any store: the
+  // stores to p / s0 / s1 may alias later loads as far as the compiler knows, which would
+  // otherwise serialise one HBM round trip per element.  Per-element arithmetic unchanged.
+  constexpr int PER = UPD_CHUNK / 256;
+  constexpr bool S0 = OPT != 1, S1 = OPT == 0 || OPT == 3 || OPT == 5;
+  float gv[PER], pv[PER], s0v[PER], s1v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = beg + threadIdx.x + 256 * j;
+    gv[j] = pv[j] = s0v[j] = s1v[j] = 0.f;
+    if (i < end) {
+      const long long k = o + i;
+      gv[j] = a.g[k];
+      pv[j] = a.p[k];
+      if constexpr (S0) s0v[j] = a.s0[k];
+      if constexpr (S1) s1v[j] = a.s1[k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = beg + threadIdx.x + 256 * j;
+    if (i >= end) continue;
     const long long k = o + i;
-    float g = a.g[k];
+    float g = gv[j];
     g = a.clip_part ? (g * 0.1f) * f : g * a.grad_scale;
-    float p = a.p[k];
+    float p = pv[j];
     if constexpr (OPT == 0) {  // ApplyAdam
-      float m = a.s0[k], v = a.s1[k];
+      float m = s0v[j], v = s1v[j];
       m += (g - m) * a.one_minus_b1;
       v += (g * g - v) * a.one_minus_b2;
       p -= (m * alpha) / (sqrtf(v) + a.eps);
@@ -394,23 +420,23 @@ __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const T
     } else if constexpr (OPT == 1) {  // ApplyGradientDescent
       p -= g * a.lr;
     } else if constexpr (OPT == 2) {  // ApplyAdagrad
-      float acc = a.s0[k] + g * g;
+      float acc = s0v[j] + g * g;
       p -= g * a.lr * rsqrtf(acc);
       a.s0[k] = acc;
     } else if constexpr (OPT == 3) {  // ApplyAdadelta
-      float acc = a.s0[k] * a.rho + g * g * a.one_minus_rho;
-      float au = a.s1[k];
+      float acc = s0v[j] * a.rho + g * g * a.one_minus_rho;
+      float au = s1v[j];
       const float upd = sqrtf(au + a.eps) * rsqrtf(acc + a.eps) * g;
       p -= upd * a.lr;
       au = au * a.rho + upd * upd * a.one_minus_rho;
       a.s0[k] = acc;
       a.s1[k] = au;
     } else if constexpr (OPT == 4) {  // ApplyMomentum (use_nesterov=False)
-      float acc = a.s0[k] * a.momentum + g;
+      float acc = s0v[j] * a.momentum + g;
       p -= acc * a.lr;
       a.s0[k] = acc;
     } else {  // ApplyRMSProp
-      float ms = a.s0[k], mom = a.s1[k];
+      float ms = s0v[j], mom = s1v[j];
       ms += (g * g - ms) * a.decay_c;
       mom = mom * a.momentum + (g * a.lr) / sqrtf(ms + a.eps);
       p -= mom;
