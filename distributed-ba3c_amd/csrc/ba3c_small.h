@@ -264,13 +264,13 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   float s = 0.f;
   if (o < MN) {
     int z = zg;
-    for (; z + 12 < S; z += 16) {
-      const float a0 = part[(size_t)z * MN + o], a1 = part[(size_t)(z + 4) * MN + o];
-      const float a2 = part[(size_t)(z + 8) * MN + o], a3 = part[(size_t)(z + 12) * MN + o];
-      s += a0;
-      s += a1;
-      s += a2;
-      s += a3;
+    // 8 slab loads in flight per thread (the adds stay in slab order: deterministic)
+    for (; z + 28 < S; z += 32) {
+      float a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = part[(size_t)(z + 4 * u) * MN + o];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += a[u];
     }
     for (; z < S; z += 4) s += part[(size_t)z * MN + o];
   }
