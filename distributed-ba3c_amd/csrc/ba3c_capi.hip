@@ -104,6 +104,14 @@ using L6Conv1D = Band6<GConv1D, 224, 128, 5>;
 // 0.44 ms at 6-row bands -> 0.31 ms: no halo re-staging, 11 m-blocks per wave hide the
 // weight-fragment latency; 6 and 9-row bands and 8-row conv1 / 12-row conv1-fwd bands measured slower)
 using L6Conv2D = Band6<BandGeom<22, 22, 64, 32, 5, 5, 18, false, 1, 8, 4, 4, 7, 7, 14, 14>, 224, 128, 11, 32>;
+// small batches (B <= SMALL_B, e.g. configs[1]'s B=32): conv2 forward / input gradient in
+// 2- / 3-row bands, so the launch has 7x / 6x the workgroups of the whole-map kernels — at
+// B=32 those are 32 workgroups on 256 CUs, one latency-bound wave of work.  Every output's
+// K order (phase, tap, channel chunk, product) is the same in both geometries, so results
+// are bit-identical across the switch.
+constexpr int SMALL_B = 128;
+using L6Conv2FS = Band6<BandGeom<18, 18, 32, 64, 5, 5, 2, true, 0, 4>, 192, 32, 2>;
+using L6Conv2DS = Band6<BandGeom<22, 22, 64, 32, 5, 5, 3, false, 1, 8, 4, 4, 7, 7, 14, 14>, 224, 128, 2, 32>;
 // weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
 using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
 using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
@@ -417,8 +425,11 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
     if (h->band) {
       CHECK(launch_bandx<L6Conv1F>(h, s, BA3C_K_CONV1_FWD,
                                      BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}, w, WT_C1F));
-      CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD,
-                                     BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B}, w, WT_C2F));
+      const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B};
+      if (h->b6 && B <= SMALL_B)
+        CHECK(launch_band6<L6Conv2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
+      else
+        CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
     } else {
       ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> c1{w.p0, W1, w.p1, w.c1, rc, 1.0f, B * 1296, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
@@ -436,8 +447,11 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
     }
     CHECK(launch_bandx<L6Conv1F>(h, s, BA3C_K_CONV1_FWD,
                                    BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}, w, WT_C1F));
-    CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD,
-                                   BandArgs{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B}, w, WT_C2F));
+    const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B};
+    if (h->b6 && B <= SMALL_B)
+      CHECK(launch_band6<L6Conv2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
+    else
+      CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
   } else {
     ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
                                                  B * 6400, 32, 25 * CH, 0};
@@ -573,7 +587,10 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
     if (h->band) {
       const BandArgs ba{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B};
-      CHECK(launch_bandx<L6Conv2D>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D));
+      if (h->b6 && B <= SMALL_B)
+        CHECK(launch_band6<L6Conv2DS>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D));
+      else
+        CHECK(launch_bandx<L6Conv2D>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D));
     } else {
       ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
