@@ -263,26 +263,31 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
   if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
 
-// fp32 [N][K] band-conv weight copies -> [3][N][K] bf16 splits (hi, mid, lo), one region
-// per job; wt6 region of job i starts at 3 * (fp32 offset of job i) bf16 elements.
-struct WSplitArgs {
-  const float* wt;
+// One launch per step for all weight preparation on the split path: job y < njobs writes the
+// bf16 splits of band-conv copy y straight from the parameters (no fp32 [N][K] copy and no
+// second pass), job y == njobs (when w0 is set) prepares conv0's MFMA B fragments.
+struct WPrep6Args {
+  WPrepArgs jobs;
   uint16_t* wt6;
-  int off[4], n[4];
-  int njobs;
+  int off[4];              // fp32 offset of job i; its splits start at 3 * off[i]
+  const float* w0;         // conv0/W (null: no conv0 job)
+  uint4* wb0;
 };
 
-__global__ void __launch_bounds__(256) wsplit_kernel(const WSplitArgs a) {
-  const int j = blockIdx.y;
-  const float* src = a.wt + a.off[j];
-  uint16_t* dst = a.wt6 + 3 * (size_t)a.off[j];
-  const int n = a.n[j];
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+__global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
+  const int y = blockIdx.y;
+  if (y == a.jobs.njobs) {
+    conv0s_wprep_one(a.w0, a.wb0, blockIdx.x * 256 + threadIdx.x);
+    return;
+  }
+  const WPrepJob& j = a.jobs.job[y];
+  uint16_t* dst = a.wt6 + 3 * (size_t)a.off[y];
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < j.n; e += gridDim.x * 256) {
     uint32_t hi, mid, lo;
-    split3(src[e], hi, mid, lo);
+    split3(wprep_value(j, e), hi, mid, lo);
     dst[e] = (uint16_t)hi;
-    dst[n + e] = (uint16_t)mid;
-    dst[2 * n + e] = (uint16_t)lo;
+    dst[j.n + e] = (uint16_t)mid;
+    dst[2 * j.n + e] = (uint16_t)lo;
   }
 }
 

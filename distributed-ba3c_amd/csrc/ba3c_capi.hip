@@ -359,26 +359,29 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
   a.job[2] = WPrepJob{W1, w.wt + WT_C1D, 5, 5, 32, 32, 1, 800 * 32};
   a.job[3] = WPrepJob{W2, w.wt + WT_C2D, 5, 5, 32, 64, 1, 1600 * 32};
   a.njobs = train ? 4 : 2;
-  hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
-  HIP_TRY(hipGetLastError());
+  const bool c0s = h->cfg.channels == 4 && h->split;
   if (h->b6) {
-    WSplitArgs sa{};
-    sa.wt = w.wt;
-    sa.wt6 = w.wt6;
+    // split path: one launch writes the bf16 splits (and conv0's fragments) directly
+    WPrep6Args pa{};
+    pa.jobs = a;
+    pa.wt6 = w.wt6;
     const int offs[4] = {WT_C1F, WT_C2F, WT_C1D, WT_C2D};
-    for (int j = 0; j < 4; ++j) {
-      sa.off[j] = offs[j];
-      sa.n[j] = a.job[j].n;
-    }
-    sa.njobs = a.njobs;
-    hipLaunchKernelGGL(wsplit_kernel, dim3(64, a.njobs), dim3(256), 0, s, sa);
+    for (int j = 0; j < 4; ++j) pa.off[j] = offs[j];
+    pa.w0 = c0s ? prm + h->tensors[h->idx_conv[0]].offset : nullptr;
+    pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
+    hipLaunchKernelGGL(wprep6_kernel, dim3(64, a.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
+    HIP_TRY(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
     HIP_TRY(hipGetLastError());
   }
-  if (h->cfg.channels == 4 && h->split) {
-    hipLaunchKernelGGL(conv0s_wprep_kernel, dim3((2 * Conv0S::KSTEPS * 64 + 255) / 256), dim3(256), 0,
-                       s, prm + h->tensors[h->idx_conv[0]].offset,
-                       reinterpret_cast<uint4*>(w.wt + WT_C0S));
-    HIP_TRY(hipGetLastError());
+  if (c0s) {
+    if (!h->b6) {
+      hipLaunchKernelGGL(conv0s_wprep_kernel, dim3((2 * Conv0S::KSTEPS * 64 + 255) / 256), dim3(256),
+                         0, s, prm + h->tensors[h->idx_conv[0]].offset,
+                         reinterpret_cast<uint4*>(w.wt + WT_C0S));
+      HIP_TRY(hipGetLastError());
+    }
   } else if (h->cfg.channels == 4) {
     hipLaunchKernelGGL(conv0_wprep_kernel, dim3((32 * Conv0Geom::KDIM + 255) / 256), dim3(256), 0, s,
                        prm + h->tensors[h->idx_conv[0]].offset, w.wt + WT_C0F);

@@ -359,22 +359,24 @@ struct WPrepArgs {
   int njobs;
 };
 
+// element e of job j's [N][K] copy (forward: [CO][KH*KW*CI]; dgrad: rotated [CI][KH*KW*CO])
+__device__ __forceinline__ float wprep_value(const WPrepJob& j, int e) {
+  if (!j.dgrad) {
+    const int K = j.KH * j.KW * j.CI;
+    const int o = e / K, k = e - o * K;            // k = (kh*KW+kw)*CI + c
+    return j.w[(size_t)k * j.CO + o];
+  }
+  const int K = j.KH * j.KW * j.CO;
+  const int ci = e / K, k = e - ci * K;            // k = (a*KW+b)*CO + o
+  const int ab = k / j.CO, o = k - ab * j.CO;
+  const int aa = ab / j.KW, bb = ab - aa * j.KW;
+  const int kh = j.KH - 1 - aa, kw = j.KW - 1 - bb;
+  return j.w[((size_t)(kh * j.KW + kw) * j.CI + ci) * j.CO + o];
+}
+
 __global__ void __launch_bounds__(256) wprep_kernel(const WPrepArgs a) {
   const WPrepJob& j = a.job[blockIdx.y];
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < j.n; e += gridDim.x * 256) {
-    if (!j.dgrad) {
-      const int K = j.KH * j.KW * j.CI;
-      const int o = e / K, k = e - o * K;            // k = (kh*KW+kw)*CI + c
-      j.wt[e] = j.w[(size_t)k * j.CO + o];
-    } else {
-      const int K = j.KH * j.KW * j.CO;
-      const int ci = e / K, k = e - ci * K;          // k = (a*KW+b)*CO + o
-      const int ab = k / j.CO, o = k - ab * j.CO;
-      const int aa = ab / j.KW, bb = ab - aa * j.KW;
-      const int kh = j.KH - 1 - aa, kw = j.KW - 1 - bb;
-      j.wt[e] = j.w[((size_t)(kh * j.KW + kw) * j.CI + ci) * j.CO + o];
-    }
-  }
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < j.n; e += gridDim.x * 256) j.wt[e] = wprep_value(j, e);
 }
 
 }  // namespace ba3c

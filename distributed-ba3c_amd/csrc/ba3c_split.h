@@ -80,10 +80,8 @@ struct Conv0S {
 
 // conv0/W [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99; real channels c < 4) -> bf16 splits
 // in MFMA B-fragment order.  One thread per (nt, kstep, lane).
-__global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restrict__ w,
-                                                           uint4* __restrict__ wb) {
+__device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, uint4* __restrict__ wb, int t) {
   using G = Conv0S;
-  const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= 2 * G::KSTEPS * 64) return;
   const int lane = t & 63, s = (t >> 6) % G::KSTEPS, nt = t / (64 * G::KSTEPS);
   const int n = nt * 16 + (lane & 15), q = lane >> 4;
@@ -99,6 +97,11 @@ __global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restri
     wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane] =
         make_uint4(part[sp][0] | (part[sp][1] << 16), part[sp][2] | (part[sp][3] << 16),
                    part[sp][4] | (part[sp][5] << 16), part[sp][6] | (part[sp][7] << 16));
+}
+
+__global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restrict__ w,
+                                                           uint4* __restrict__ wb) {
+  conv0s_wprep_one(w, wb, blockIdx.x * 256 + threadIdx.x);
 }
 
 // Persistent workgroups walk bands (one image x RB output rows = RB/2 pooled rows); wave w
