@@ -272,10 +272,13 @@ struct WPrep6Args {
   int off[4];              // fp32 offset of job i; its splits start at 3 * off[i]
   const float* w0;         // conv0/W (null: no conv0 job)
   uint4* wb0;
+  unsigned long long* relu;  // training: ReLU-count slots zeroed here (no separate memset)
 };
 
 __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
   const int y = blockIdx.y;
+  if (y == 0 && a.relu)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < RELU_SLOTS; i += gridDim.x * 256) a.relu[i] = 0ull;
   if (y == a.jobs.njobs) {
     conv0s_wprep_one(a.w0, a.wb0, blockIdx.x * 256 + threadIdx.x);
     return;

@@ -369,6 +369,7 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
     for (int j = 0; j < 4; ++j) pa.off[j] = offs[j];
     pa.w0 = c0s ? prm + h->tensors[h->idx_conv[0]].offset : nullptr;
     pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
+    pa.relu = train ? w.relu : nullptr;
     hipLaunchKernelGGL(wprep6_kernel, dim3(64, a.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
     HIP_TRY(hipGetLastError());
   } else {
@@ -873,7 +874,8 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
   CHECK(ensure_side_stream(h, s));
   Workspace w = carve(h, workspace, batch, true);
   HIP_TRY(hipMemsetAsync(grads, 0, (size_t)h->flat * 4, s));
-  HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_SLOTS * 8, s));
+  // on the band + split path the weight-prep launch zeroes the ReLU counters
+  if (!(h->band && h->b6)) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_SLOTS * 8, s));
   int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, true)
                                : run_forward<12>(h, s, params, state, batch, w, true);
   if (r != BA3C_OK) return r;
