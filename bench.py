@@ -71,10 +71,10 @@ def build_trainer(B, F, S, A, world, seed):
     from ba3c_amd.model import Model
     from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
     from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
-    from oracle.ba3c_oracle import init_params  # weight initialiser only (numpy RNG)
 
-    model = Model(num_actions=A, channels=1, fc_neurons=F, fc_splits=S, batch_size=B, max_batch=B)
-    model.engine.load_params(init_params(F, S, A, seed=0, dtype=np.float32))
+    # reference initialisers (conv2d.py:48-55, fc.py:35-38) from the product package, seed 0
+    model = Model(num_actions=A, channels=1, fc_neurons=F, fc_splits=S, batch_size=B, max_batch=B,
+                  seed=0)
     opt = AdamOptimizer(1e-3, beta1=0.8, beta2=0.75, epsilon=1e-8)   # README.md:35
     if world > 1:
         opt = SyncReplicasOptimizer(opt, replicas_to_aggregate=world, total_num_replicas=world)
@@ -94,24 +94,28 @@ def sync_all(world):
 
 
 def time_steps(tr, batch, steps, warmup, world, probe=None):
+    """Time exactly `steps` steps bracketed by barrier + synchronize (max over ranks), and
+    each step's own HIP-event interval on the learner stream (for the median)."""
     for _ in range(warmup):
         tr.train_step(*batch)
     sync_all(world)
     if probe is not None:
         tr.engine.probe_enable(probe)   # bracket the dominant kernel over the timed steps only
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    for _ in range(steps):
+    evs[0].record()
+    for i in range(steps):
         tr.train_step(*batch)
-    ev1.record()
+        evs[i + 1].record()
     sync_all(world)
     wall = time.perf_counter() - t0
-    gpu_s = ev0.elapsed_time(ev1) / 1000.0
-    el = torch.tensor([max(wall, gpu_s)], dtype=torch.float64, device="cuda")
+    per_step = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    gpu_s = sum(per_step) / 1000.0
+    el = torch.tensor([max(wall, gpu_s), float(np.median(per_step))], dtype=torch.float64,
+                      device="cuda")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    return float(el.item())
+    return float(el[0].item()), float(el[1].item())
 
 
 def time_graph_steps(tr, batch, steps, warmup):
@@ -194,41 +198,64 @@ def find_dominant_kernel(tr, batch):
     return best, per
 
 
-def cpu_baseline(F, S, A, seconds=12.0):
-    """The oracle (numpy float32 restatement of the TF graph incl. 16-channel padding, TF clip,
-    TF Adam) timed on this host on a bounded sample: steps of B=16 frames until ~`seconds`."""
-    from oracle import ba3c_oracle as O
+def cpu_threads():
+    """Threads the CPU baseline may use: the process's CPU share (OMP_NUM_THREADS on the GPU
+    box, else the CPUs this process may run on)."""
+    n = os.environ.get("OMP_NUM_THREADS")
+    if n and n.isdigit() and int(n) > 0:
+        return int(n)
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    rs = np.random.RandomState(0)
-    B = 16
-    params = O.init_params(F, S, A, seed=0, dtype=np.float32)
-    slots = O.init_slots(params, "adam", 0.8, 0.75)
-    cfg = {"fc_neurons": F, "fc_splits": S}
-    state = rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)
-    action = rs.randint(0, A, size=B).astype(np.int64)
-    R = rs.normal(size=B).astype(np.float32)
-    O.train_step(params, slots, 1, [(state, action, R)], cfg, lr=1e-3, beta1=0.8, beta2=0.75)
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        params, slots, _, _ = O.train_step(params, slots, 1, [(state, action, R)], cfg, lr=1e-3,
-                                           beta1=0.8, beta2=0.75)
-        n += 1
-    dt = time.perf_counter() - t0
-    cpu = "unknown"
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": round(n * B / dt, 2), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": "%d numpy-fp32 oracle train steps of B=%d (F=%d, S=%d) in %.1f s on %s"
-                      % (n, B, F, S, dt, cpu)}
+    return "unknown CPU"
+
+
+def cpu_baseline(F, S, A, big_seconds=10.0, b32_steps=50):
+    """SURVEY.md §8d / BASELINE.md §2: the PyTorch-CPU fp32 restatement of the reference TF
+    graph (oracle/ba3c_torch_cpu.py: 16-channel padding, log-eps loss, autodiff, TF clip, TF
+    Adam) timed on this host's cores beside the GPU: the bench workload (B=2048, F, S) for a
+    bounded number of steps (>= 2, ~`big_seconds`) and configs[1] (B=32, F=128, S=4) for
+    `b32_steps` steps; median step time of each."""
+    from oracle import ba3c_oracle as O
+    from oracle.ba3c_torch_cpu import TorchCpuBa3c
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+
+    def run(B, F_, S_, min_steps, max_steps, seconds, warm):
+        rs = np.random.RandomState(0)
+        m = TorchCpuBa3c(O.init_params(F_, S_, A, seed=0, dtype=np.float32), F_, S_)
+        st = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8))
+        ac = torch.from_numpy(rs.randint(0, A, size=B).astype(np.int64))
+        R = torch.from_numpy(rs.normal(size=B).astype(np.float32))
+        for _ in range(warm):
+            m.step(st, ac, R)
+        ts = []
+        t_all = time.perf_counter()
+        while len(ts) < max_steps and (len(ts) < min_steps or time.perf_counter() - t_all < seconds):
+            t0 = time.perf_counter()
+            m.step(st, ac, R)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), len(ts)
+
+    big_med, big_n = run(2048, F, S, 2, 20, big_seconds, 1)
+    small_med, small_n = run(32, 128, 4, b32_steps, b32_steps, 0.0, 3)
+    return {"value": round(2048 / big_med, 2), "unit": "samples/s", "cores": threads,
+            "kind": "port",
+            "sample": "PyTorch-CPU fp32 restatement of the reference TF graph (oracle/ba3c_torch_cpu.py),"
+                      " %d threads on %s: B=2048 F=%d S=%d median of %d steps (%.2f s/step); "
+                      "configs[1] B=32 F=128 S=4 median of %d steps" % (
+                          threads, cpu_model(), F, S, big_n, big_med, small_n),
+            "b32_value": round(32 / small_med, 2), "b32_ms_per_step": round(small_med * 1000, 2)}
 
 
 def main():
@@ -244,7 +271,7 @@ def main():
     ap.add_argument("--no-b32", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--predict_batch", type=int, default=8192)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -265,7 +292,7 @@ def main():
     dom, per_kernel = find_dominant_kernel(tr, batch)
     sync_all(world)
 
-    elapsed = time_steps(tr, batch, args.steps, args.warmup, world, probe=dom)
+    elapsed, med_ms = time_steps(tr, batch, args.steps, args.warmup, world, probe=dom)
     probe_ms, launches = tr.engine.probe_read()
     tr.engine.probe_enable(None)
 
@@ -293,6 +320,8 @@ def main():
 
     out = {"metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+           "ms_per_step_median": round(med_ms, 4),
+           "value_median": round(world * B / (med_ms / 1000.0), 1),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "data": "synthetic uint8 84x84x4 frames, random actions/returns, weights from the "
                    "reference initialisers (seed 0); resident in HBM",
@@ -313,16 +342,18 @@ def main():
         del tr
         tr32, b32 = build_trainer(32, 128, 4, A, world, seed=rank)
         n32 = max(args.steps, 100)
-        el32 = time_steps(tr32, b32, n32, 10, world)
+        el32, med32 = time_steps(tr32, b32, n32, 10, world)
         out["b32"] = {"config": "configs[1]: B=32/GPU, fc_neurons=128, fc_splits=4",
                       "value": round(world * 32 * n32 / el32, 1), "unit": "samples/s",
-                      "ms_per_step": round(el32 / n32 * 1000.0, 4), "launch": "eager"}
+                      "ms_per_step": round(el32 / n32 * 1000.0, 4),
+                      "ms_per_step_median": round(med32, 4), "launch": "eager"}
         if world == 1:
             elg = time_graph_steps(tr32, b32, n32, 10)
             out["b32"].update({"value_graph": round(32 * n32 / elg, 1),
                                "ms_per_step_graph": round(elg / n32 * 1000.0, 4)})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(F, S, A, args.cpu_seconds)
+        out["gpu_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -73,6 +73,7 @@ def load():
         "ba3c_apply_update_dev": (i32, [P, P, i32, P, P, P, P, ctypes.POINTER(Ba3cOptParams), P,
                                         f32, i32, P]),
         "ba3c_sample": (i32, [P, P, P, i32, i32, P, P]),
+        "ba3c_greedy": (i32, [P, P, P, P, i32, i32, ctypes.c_double, P]),
         "ba3c_probe_enable": (i32, [P, i32]),
         "ba3c_probe_read": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]),
         "ba3c_kernel_split": (i32, [P, i32]),

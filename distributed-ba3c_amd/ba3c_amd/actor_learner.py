@@ -60,7 +60,11 @@ class ActorLearner(object):
     """The loop above around an existing Ba3cTrainer (whose model engine also serves as the
     predictor: the reference's towerp0 reads the same variables, train.py:355-362)."""
 
-    def __init__(self, trainer, n_envs, batch_size, seed=0, rs=None):
+    def __init__(self, trainer, n_envs, batch_size, seed=0, rs=None, on_train_step=None,
+                 dummy_predictor=False):
+        """on_train_step(trainer): called after every learner step (callbacks / metrics);
+        dummy_predictor: --dummy_predictor 1 (predict/base.py:94-105) — uniform policy and
+        U(0,1) values instead of the network forward."""
         eng = trainer.engine
         assert eng.channels == 4, "synthetic loop is grayscale x FRAME_HISTORY=4"
         self.trainer = trainer
@@ -74,11 +78,23 @@ class ActorLearner(object):
         self.steps = 0
         self.train_steps = 0
         self.last_scalars = None
+        self.on_train_step = on_train_step
+        self.dummy_predictor = dummy_predictor
+
+    def _predict(self, state):
+        eng = self.engine
+        if self.dummy_predictor:
+            E, A = self.env.E, eng.num_actions
+            probs = torch.full((E, A), 1.0 / A, dtype=torch.float32, device=eng.device)
+            value = torch.from_numpy(self.rs.uniform(size=E).astype(np.float32)).to(eng.device)
+            return probs, value
+        _, probsT, value = eng.forward(state, explore_factor=self.trainer.model.explore_factor)
+        return probsT, value
 
     def iterate(self):
         eng = self.engine
         state = self.hist.state
-        _, probsT, value = eng.forward(state, explore_factor=self.trainer.model.explore_factor)
+        probsT, value = self._predict(state)
         u = torch.from_numpy(self.rs.random_sample(self.env.E)).to(eng.device)
         actions, flag = eng.sample(probsT, u)
         self.buf.on_state(state, actions, value)
@@ -92,6 +108,8 @@ class ActorLearner(object):
             self.trainer.train_step(b[0].contiguous(), b[1].contiguous(), b[2].contiguous())
             self.train_steps += 1
             self.last_scalars = self.trainer.model.scalars
+            if self.on_train_step is not None:
+                self.on_train_step(self.trainer)
         self.steps += 1
         if int(flag.item()) & 1:
             raise AssertionError("non-finite action distribution (train.py:381)")

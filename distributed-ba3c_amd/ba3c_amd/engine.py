@@ -85,6 +85,13 @@ class Ba3cEngine(object):
             assert v.shape == shape, (n, v.shape, shape)
             self.params[off:off + numel].copy_(torch.from_numpy(v.reshape(-1)))
 
+    def init_params(self, seed=0, conv_init="normal", fc_init="uniform"):
+        """Fresh variables with the reference's initialisers (initializers.py)."""
+        from .initializers import initial_values
+        self.load_params(initial_values(self.layout, seed=seed, conv_init=conv_init,
+                                        fc_init=fc_init,
+                                        replace_with_conv=self.cfg["replace_with_conv"]))
+
     def state_dict(self, flat=None):
         flat = self.params if flat is None else flat
         host = flat.detach().cpu().numpy()
@@ -188,6 +195,18 @@ class Ba3cEngine(object):
         _lib.check(self.lib.ba3c_sample(_stream(), _ptr(probs.contiguous()), _ptr(u), B, A,
                                         _ptr(actions), _ptr(flag)))
         return actions, flag
+
+    def greedy(self, probs, u, random_actions, eps=0.001, actions=None):
+        """Evaluation action: first argmax of each row, random_actions[i] where u[i] < eps."""
+        B, A = probs.shape
+        assert u.dtype == torch.float64 and u.shape == (B,)
+        assert random_actions.dtype == torch.int64 and random_actions.shape == (B,)
+        if actions is None:
+            actions = torch.empty(B, dtype=torch.int64, device=probs.device)
+        _lib.check(self.lib.ba3c_greedy(_stream(), _ptr(probs.contiguous()), _ptr(u),
+                                        _ptr(random_actions.contiguous()), B, A, float(eps),
+                                        _ptr(actions)))
+        return actions
 
     # -- timing probe -------------------------------------------------------------------
     def probe_enable(self, kernel):

@@ -22,16 +22,22 @@ GAMMA = 0.99              # train.py:94
 
 class Model(ModelDesc):
     def __init__(self, num_actions, channels=1, fc_neurons=512, fc_splits=1,
-                 replace_with_conv=True, ps=1, batch_size=128, max_batch=None, engine=None):
+                 replace_with_conv=True, ps=1, batch_size=128, max_batch=None, engine=None,
+                 seed=0, conv_init="normal", fc_init="uniform"):
         """channels: the reference's --channels (frames per history step; CHANNEL =
-        FRAME_HISTORY*channels, train.py:95).  BASELINE's 84x84x4 input is channels=1."""
+        FRAME_HISTORY*channels, train.py:95).  BASELINE's 84x84x4 input is channels=1.
+        A new engine starts from the reference initialisers (--conv_init / --fc_init,
+        initializers.py) drawn with `seed`; a caller-supplied engine keeps its variables."""
         self.num_actions = num_actions
         self.channel = FRAME_HISTORY * channels
         self.batch_size = batch_size
-        self.engine = engine or Ba3cEngine(num_actions=num_actions, channels=self.channel,
-                                           fc_neurons=fc_neurons, fc_splits=fc_splits,
-                                           replace_with_conv=replace_with_conv, ps=ps,
-                                           max_batch=max_batch or max(batch_size, 16))
+        if engine is None:
+            engine = Ba3cEngine(num_actions=num_actions, channels=self.channel,
+                                fc_neurons=fc_neurons, fc_splits=fc_splits,
+                                replace_with_conv=replace_with_conv, ps=ps,
+                                max_batch=max_batch or max(batch_size, 16))
+            engine.init_params(seed=seed, conv_init=conv_init, fc_init=fc_init)
+        self.engine = engine
         self.entropy_beta = 0.01      # non-trainable var 'entropy_beta' (train.py:296-297)
         self.explore_factor = 1.0     # non-trainable var 'explore_factor' (train.py:294-295)
         self.vars_for_save = {n: n for n in self.engine.tensor_names}

@@ -182,7 +182,8 @@ class SyncReplicasOptimizer(object):
     def __init__(self, opt, replicas_to_aggregate=None, total_num_replicas=None, group=None):
         self._opt = opt
         self.group = group
-        world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.distributed = dist.is_available() and dist.is_initialized()
+        world = dist.get_world_size(group) if self.distributed else 1
         self.total_num_replicas = total_num_replicas or world
         self.replicas_to_aggregate = replicas_to_aggregate or self.total_num_replicas
         if self.total_num_replicas != world or self.replicas_to_aggregate != world:
@@ -199,11 +200,34 @@ class SyncReplicasOptimizer(object):
     def learning_rate(self, v):
         self._opt.learning_rate = v
 
+    @property
+    def slots(self):
+        return self._opt.slots
+
+    def powers(self):
+        return self._opt.powers()
+
+    def broadcast_variables(self, engine, src=0):
+        """Every replica starts from rank `src`'s variables (and optimizer slots, e.g. after a
+        restore), as all workers of the reference read the one PS copy (train.py:512-515)."""
+        if not self.distributed:
+            return
+        dist.broadcast(engine.params, src=src, group=self.group)
+        for t in (self._opt.slots or []):
+            dist.broadcast(t, src=src, group=self.group)
+        if self._opt.dev_powers is not None:
+            dist.broadcast(self._opt.dev_powers, src=src, group=self.group)
+
+    def allreduce(self, engine):
+        """Sum of the replicas' flat gradient buffers over RCCL ('nccl' backend), issued on the
+        current HIP stream; runs whenever a process group exists (also at world size 1)."""
+        if self.distributed:
+            dist.all_reduce(engine.grads, op=dist.ReduceOp.SUM, group=self.group)
+
     def aggregate(self, engine):
         """Per-replica clip (multigpu.py:157) then the RCCL sum of the clipped buffer."""
         engine.clip_grads()
-        if self.world > 1:
-            dist.all_reduce(engine.grads, op=dist.ReduceOp.SUM, group=self.group)
+        self.allreduce(engine)
 
     def apply_gradients(self, engine):
         self._opt.apply_gradients(engine, grad_scale=1.0 / self.world, fuse_clip=False)

@@ -42,6 +42,8 @@ class Ba3cTrainer(object):
                             and isinstance(procs[0].func, ClipByAverageNorm)
                             and procs[0].regex == ".*$")
         self._procs = procs
+        if isinstance(self.optimizer, SyncReplicasOptimizer):
+            self.optimizer.broadcast_variables(self.engine)
 
     def process_grads(self):
         for p in self._procs:
@@ -56,8 +58,7 @@ class Ba3cTrainer(object):
                 opt.aggregate(self.engine)
             else:
                 self.process_grads()
-                if opt.world > 1:
-                    torch.distributed.all_reduce(self.engine.grads)
+                opt.allreduce(self.engine)
             opt.apply_gradients(self.engine)
         elif self._fused_clip:
             opt.apply_gradients(self.engine, fuse_clip=True)
@@ -70,17 +71,29 @@ class Ba3cTrainer(object):
         """Capture one full step (fwd+bwd+clip+update) on static input tensors as a hipGraph
         (torch.cuda.CUDAGraph over the HIP stream).  Returns a callable that replays it; the
         caller refills `state`/`action`/`futurereward` in place between replays.  Adam's
-        beta powers move to the device so every replay uses the right bias correction."""
+        beta powers move to the device so every replay uses the right bias correction.
+        The `warmup` eager steps that precede the capture (allocator / library warm-up) are
+        undone: parameters, optimizer slots and beta powers are restored afterwards, so
+        capturing does not train the model."""
         opt = self.optimizer
         inner = opt._opt if isinstance(opt, SyncReplicasOptimizer) else opt
         if hasattr(inner, "use_device_state"):
             inner.use_device_state(self.engine.device)
+        if inner.slots is None:
+            inner.slots = inner._init_slots(self.engine)
+        saved = [t.clone() for t in [self.engine.params] + list(inner.slots)
+                 + ([inner.dev_powers] if inner.dev_powers is not None else [])]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self.train_step(state, action, futurereward)
+            live = [self.engine.params] + list(inner.slots) + (
+                [inner.dev_powers] if inner.dev_powers is not None else [])
+            for dst, src in zip(live, saved):
+                dst.copy_(src)
         torch.cuda.current_stream().wait_stream(side)
+        self.global_step -= warmup
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             self.train_step(state, action, futurereward)

@@ -54,7 +54,6 @@ struct Band6Args {
   uint8_t* out_code;       // POOL: argmax codes (may be null: predictor)
   unsigned long long* relu_count;
   int batch;
-  int dbg;                 // profiling only: bit0 skip staging loads, bit1 skip the MFMA loop
 };
 
 template <class L>
@@ -91,7 +90,6 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
         const unsigned f = tid + 256u * (base + i);
         const unsigned pix = f / Q, cq = f - pix * Q;
         v[i] = f4zero();
-        if (a.dbg & 1) continue;
         if constexpr (G::SRC == 0) {
           if (f < nvec) v[i] = *reinterpret_cast<const float4*>(srcb + pix * G::CIN + cq * 4);
         } else {
@@ -188,7 +186,6 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
     for (int t = 0; t < LA && t < L::NT; ++t)
 #pragma unroll
       for (int s = 0; s < 3; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
-    if (a.dbg & 2) continue;
 #pragma unroll
     for (int t = 0; t < L::NT; ++t) {
       if (t + LA < L::NT) {

@@ -71,7 +71,6 @@ struct ba3c_handle {
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
-  int dbg = 0;        // BA3C_DBG: profiling-only kernel ablations (results are wrong when set)
   // backward weight gradients on a side stream (BA3C_OVERLAP=1; created on the first training
   // call that is not being captured). Off by default: r01t/u measured +0.5% step throughput
   // (561k vs 557k samples/s) because conv1's dgrad and wgrad kernels each fill the chip, and
@@ -199,6 +198,9 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   };
   const size_t Bz = (size_t)B;
   const int F = h->cfg.fc_neurons;
+  // The clip / optimizer per-chunk sum-of-squares partials come FIRST, at a batch-independent
+  // offset: ba3c_clip_grads / ba3c_apply_update receive only the workspace base.
+  w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
   w.p0 = (float*)take(Bz * P0 * 4);
   w.p1 = (float*)take(Bz * P1 * 4);
   w.p2 = (float*)take(Bz * P2 * 4);
@@ -221,9 +223,6 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
     w.terms = (float*)take(Bz * NTERMS * 4);
     w.part = (float*)take(max_partials(h, B) * 4);
     w.part0 = (float*)take(max_partials0(h, B) * 4);
-    w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
-  } else {
-    w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
   }
   w.bytes = off;
   return w;
@@ -290,8 +289,7 @@ int launch_band(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a) {
 template <class L>
 int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
                  int wt_off) {
-  const Band6Args b{a.src, a.code, w.wt6 + 3 * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch,
-                    h->dbg};
+  const Band6Args b{a.src, a.code, w.wt6 + 3 * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch};
   dim3 grid(a.batch * L::G::NBANDS);
   {
     ProbeScope ps(h, s, kid);
@@ -725,7 +723,6 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_DBG")) h->dbg = atoi(e);
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = (e[0] == '1');
 
   const int F = c.fc_neurons, per = F / splits;
@@ -893,7 +890,7 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
 int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace) {
   if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  float* part = static_cast<float*>(workspace);  // first nchunks floats of any workspace
+  float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
   {
     ProbeScope ps(h, s, BA3C_K_CLIP);
     hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part);
@@ -931,7 +928,7 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
   a.momentum = hp->momentum;
   a.rho = hp->rho;
   a.one_minus_rho = 1.0f - hp->rho;
-  float* part = static_cast<float*>(workspace);
+  float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
   if (fuse_clip) {
     hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part);
     HIP_TRY(hipGetLastError());
@@ -983,6 +980,18 @@ int ba3c_sample(void* stream, const float* probs, const double* u, int32_t batch
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(sample_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, probs, u, batch,
                      num_actions, actions, nonfinite);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_greedy(void* stream, const float* probs, const double* u, const int64_t* random_actions,
+                int32_t batch, int32_t num_actions, double eps, int64_t* actions) {
+  if (batch < 0 || num_actions < 1) return fail(BA3C_ERR_INVALID, "bad shape");
+  if (batch == 0) return BA3C_OK;
+  if (!probs || !u || !random_actions || !actions) return fail(BA3C_ERR_INVALID, "null pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(greedy_kernel, dim3((batch + 255) / 256), dim3(256), 0, s, probs, u, random_actions,
+                     batch, num_actions, eps, actions);
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }

@@ -477,4 +477,26 @@ __global__ void __launch_bounds__(256) sample_kernel(const float* __restrict__ p
   if (bad && flag) atomicOr(flag, bad);
 }
 
+// Evaluation players' action (OpenAIGym/common.py:24-33): numpy argmax of the policy (first
+// maximum; a NaN counts as the maximum, first NaN wins, as np.argmax), replaced by the action
+// space's random sample where the player's uniform draw is below eps.
+__global__ void __launch_bounds__(256) greedy_kernel(const float* __restrict__ probs,
+                                                     const double* __restrict__ u,
+                                                     const int64_t* __restrict__ rand_act, int B,
+                                                     int A, double eps, int64_t* __restrict__ actions) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= B) return;
+  const float* pn = probs + (size_t)n * A;
+  float best = pn[0];
+  int arg = 0;
+  for (int k = 1; k < A && !isnan(best); ++k) {
+    const float v = pn[k];
+    if (isnan(v) || v > best) {
+      best = v;
+      arg = k;
+    }
+  }
+  actions[n] = u[n] < eps ? rand_act[n] : (int64_t)arg;
+}
+
 }  // namespace ba3c

@@ -166,6 +166,12 @@ int ba3c_apply_update_dev(ba3c_handle* h, void* stream, int32_t opt, float* para
 int ba3c_sample(void* stream, const float* probs, const double* u, int32_t batch,
                 int32_t num_actions, int64_t* actions, int32_t* nonfinite);
 
+/* Evaluation action (OpenAIGym/common.py:24-33, play_one_episode): actions[i] = first argmax of
+ * probs[i] (np.argmax), or random_actions[i] (the player's action_space.sample()) when
+ * u[i] < eps (`random.random() < 0.001`). */
+int ba3c_greedy(void* stream, const float* probs, const double* u, const int64_t* random_actions,
+                int32_t batch, int32_t num_actions, double eps, int64_t* actions);
+
 /* Timing probe: bracket every launch of kernel `kernel_id` with HIP events (on the stream
  * it is launched on) until disabled (kernel_id = -1).  ba3c_probe_read synchronises the
  * recorded events and returns the summed milliseconds and launch count since enabling. */

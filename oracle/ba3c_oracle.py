@@ -364,6 +364,45 @@ def loss_and_grads(params, state, action, futurereward, cfg, entropy_beta=0.01, 
     return t, scalars, grads
 
 
+def loss_and_grads_chunked(params, state, action, futurereward, cfg, entropy_beta=0.01,
+                           forced=None, chunk=16):
+    """loss_and_grads over a large batch evaluated in sub-batches of <= `chunk` samples (memory
+    stays at one chunk's im2col).  The cost is a mean over the batch (train.py:299,326-327), so
+    the full-batch gradient is sum_c (B_c/B) grad_c, and the scalars combine the same way
+    (means weighted, max_logit maxed, active_relus summed).  Returns (t, scalars, grads) with t
+    holding the per-sample outputs ('logits', 'pred_value') and the oracle's own discrete
+    decisions ('own_c0'..'own_c2': argmax codes with 255 where the window max <= 0, 'a3_pos')."""
+    B = state.shape[0]
+    dt = params["conv0/W"].dtype
+    grads, sc = None, None
+    keep = {"logits": [], "pred_value": [], "own_c0": [], "own_c1": [], "own_c2": [], "a3_pos": []}
+    for lo in range(0, B, chunk):
+        hi = min(B, lo + chunk)
+        f = None if forced is None else {k: v[lo:hi] for k, v in forced.items()}
+        t, s, g = loss_and_grads(params, state[lo:hi], action[lo:hi], futurereward[lo:hi], cfg,
+                                 entropy_beta, forced=f)
+        w = dt.type(hi - lo) / dt.type(B)
+        if grads is None:
+            grads = {k: v * w for k, v in g.items()}
+            sc = {k: (v if k in ("max_logit", "active_relus") else v * w) for k, v in s.items()}
+        else:
+            for k in g:
+                grads[k] = grads[k] + g[k] * w
+            for k, v in s.items():
+                if k == "max_logit":
+                    sc[k] = max(sc[k], v)
+                elif k == "active_relus":
+                    sc[k] += v
+                else:
+                    sc[k] = sc[k] + v * w
+        keep["logits"].append(t["logits"])
+        keep["pred_value"].append(t["pred_value"])
+        for layer in range(3):
+            keep["own_c%d" % layer].append(np.where(t["p%d" % layer] > 0, t["c%d" % layer], 255))
+        keep["a3_pos"].append(t["a3"] > 0)
+    return {k: np.concatenate(v) for k, v in keep.items()}, sc, grads
+
+
 # --- gradient processor (train.py:329-330, tfutils/gradproc.py:34-67) --------------------
 def clip_by_average_norm(g, clip_norm=CLIP_NORM):
     """tf.clip_by_average_norm (Appendix A.9): (t*c) * min(rsqrt(sum t^2) * n, 1/c)."""

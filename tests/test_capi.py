@@ -90,3 +90,36 @@ def test_entry_points_reject_null_pointers_without_gpu():
     r = lib.ba3c_forward(h, None, None, None, 4, 1.0, None, None, None, None)
     assert r == 1
     lib.ba3c_destroy(h)
+
+
+def test_clip_partials_do_not_alias_activations():
+    """The clip / optimizer sum-of-squares partials sit in a batch-independent first region of
+    every workspace: no intermediate tensor starts before it ends."""
+    L, lib, st, h = _create()
+    assert st == 0
+    for train in (0, 1):
+        for B in (1, 32):
+            off, nb = ctypes.c_int64(), ctypes.c_int64()
+            assert lib.ba3c_workspace_tensor(h, B, train, b"p0", ctypes.byref(off), ctypes.byref(nb)) == 0
+            assert off.value >= 256
+    lib.ba3c_destroy(h)
+
+
+@pytest.mark.parametrize("F,S,legacy,ps,conv_init,fc_init",
+                         [(128, 4, False, 1, "normal", "uniform"), (512, 1, False, 1, "xavier", "normal"),
+                          (256, 1, True, 4, "uniform", "uniform")])
+def test_product_initialisers_match_oracle_restatement(F, S, legacy, ps, conv_init, fc_init):
+    """ba3c_amd.initializers (conv2d.py:48-55, fc.py:35-38) draws, for a layout and seed, the
+    same values as the oracle's independent restatement."""
+    from ba3c_amd.initializers import initial_values
+    L, lib, st, h = _create(fc_neurons=F, fc_splits=S, replace_with_conv=0 if legacy else 1, ps=ps)
+    lay = _layout(lib, h)
+    lib.ba3c_destroy(h)
+    got = initial_values(lay, seed=3, conv_init=conv_init, fc_init=fc_init,
+                         replace_with_conv=not legacy)
+    ref = O.init_params(F, S, 4, seed=3, conv_init=conv_init, fc_init=fc_init,
+                        replace_with_conv=not legacy, ps=ps)
+    assert list(got) == list(ref)
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k])
+    assert np.abs(got["conv1/W"]).max() <= (0.06 if conv_init == "normal" else 0.2)

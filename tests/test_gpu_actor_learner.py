@@ -53,3 +53,26 @@ def test_actor_learner_runs_and_feeds_the_reference_datapoints():
     assert not torch.equal(m.engine.params, p0)
     want = [(k["action"], float(np.float32(R))) for k, R, _, _ in mirror.queue]
     assert consumed == want and len(want) >= B * loop.train_steps
+
+
+def test_launcher_runs_sync_training_and_saves_a_checkpoint(tmp_path):
+    """`python -m ba3c_amd.train` on the README's best flags (run_job.py -o adam --use_sync
+    -b 32 --fc_neurons 128 --fc_splits 4 --beta1 0.8 --beta2 0.75), one GPU = world size 1:
+    the actor-learner loop trains 6 steps through SyncReplicasOptimizer's RCCL all-reduce,
+    writes the metrics channels and a ModelSaver checkpoint that --load restores."""
+    from ba3c_amd.train import main
+    argv = ("-o adam --use_sync -g 1 -l 0.001 -b 32 --fc_neurons 128 --fc_splits 4 "
+            "--epsilon 1e-8 --beta1 0.8 --beta2 0.75 --simulator_procs 64 --max_steps 6 "
+            "--send_debug_every 3 --save_every 6").split()
+    argv += ["--models_dir", str(tmp_path / "models"), "--experiment_dir", str(tmp_path / "exp")]
+    out = main(argv)
+    assert out["global_step"] >= 6 and out["last"] is not None
+    assert np.isfinite(out["last"]["cost"])
+    ckpts = list((tmp_path / "models").rglob("*.npz"))
+    assert len(ckpts) == 1
+    with np.load(str(ckpts[0]), allow_pickle=False) as f:
+        assert "conv0/W" in f.files and "conv0/W/Adam" in f.files and int(f["global_step"]) == 6
+    assert any((tmp_path / "exp").iterdir())
+    out2 = main(argv[:-4] + ["--max_steps", "8", "--load", str(ckpts[0]),
+                             "--models_dir", str(tmp_path / "m2"), "--experiment_dir", str(tmp_path / "e2")])
+    assert out2["global_step"] >= 8

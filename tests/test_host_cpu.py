@@ -162,3 +162,23 @@ def test_product_engine_fails_loudly_without_gpu():
     from ba3c_amd.engine import Ba3cEngine
     with pytest.raises(Ba3cLibraryError):
         Ba3cEngine(num_actions=4, fc_neurons=128, fc_splits=4, max_batch=4)
+
+
+def test_launcher_flags_build_the_reference_configuration():
+    """`python -m ba3c_amd.train` reads run_job.py's flags into the model geometry, the
+    optimizer and the sync-replica rule (train.py:582-606, run_job.py:13-57)."""
+    from ba3c_amd.flags import build_parser, resolve
+    from ba3c_amd.train import check_distributed, model_config, optimizer_config
+    a = resolve(build_parser().parse_args(
+        "-n 71 -g 2 -c 12 -o adam --use_sync -l 0.001 -b 32 --fc_neurons 128 --simulator_procs 10 "
+        "--ps 4 --fc_splits 4 --epsilon 1e-8 --beta1 0.8 --beta2 0.75 -e Breakout-v0".split()))
+    assert model_config(a) == dict(num_actions=4, channels=1, fc_neurons=128, fc_splits=4,
+                                   replace_with_conv=True, ps=4, batch_size=32)
+    assert optimizer_config(a) == dict(name="adam", lr=0.001, beta1=0.8, beta2=0.75, epsilon=1e-8)
+    check_distributed(a, 2)
+    with pytest.raises(SystemExit):
+        check_distributed(a, 4)              # --ngrads must equal the GPU process count
+    b = resolve(build_parser().parse_args("-b 32 -o rms".split()))
+    check_distributed(b, 1)
+    with pytest.raises(SystemExit):
+        check_distributed(b, 2)              # no asynchronous multi-GPU mode

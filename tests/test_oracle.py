@@ -169,3 +169,49 @@ def test_train_step_sync_mean_of_clipped():
         exp = (O.clip_by_average_norm(g0[k]) + O.clip_by_average_norm(g1[k])) / np.float32(2)
         np.testing.assert_allclose(g[k], exp, rtol=1e-6, atol=1e-12)
     assert news["beta1_power"] == np.float32(np.float32(0.8) * np.float32(0.8))
+
+
+def test_chunked_oracle_equals_whole_batch():
+    """loss_and_grads_chunked (used to pin large-batch GPU steps) reproduces the whole-batch
+    oracle: gradients and scalars combine by the batch-mean weights of train.py:299,326."""
+    params, state, action, R = _small_case(seed=4, B=7, scale=2.0)
+    _, sc, g = O.loss_and_grads(params, state, action, R, CFG)
+    t2, sc2, g2 = O.loss_and_grads_chunked(params, state, action, R, CFG, chunk=3)
+    for k in g:
+        np.testing.assert_allclose(g2[k], g[k], rtol=1e-11, atol=1e-15)
+    for k in sc:
+        assert abs(float(sc2[k]) - float(sc[k])) <= 1e-11 * max(1.0, abs(float(sc[k]))), k
+    assert t2["logits"].shape == (7, 4) and t2["own_c0"].shape == (7, 40, 40, 32)
+
+
+def test_torch_cpu_baseline_restatement_matches_oracle():
+    """oracle/ba3c_torch_cpu.py (the timed CPU baseline) computes the same step as the numpy
+    oracle: raw gradients within 1e-4 and one clip+Adam update within 1e-4 of the update."""
+    from oracle.ba3c_torch_cpu import TorchCpuBa3c
+    cfg = {"fc_neurons": 16, "fc_splits": 2}
+    p32 = O.init_params(16, 2, 4, seed=2, dtype=np.float32)
+    for k in p32:
+        p32[k] = p32[k] * np.float32(2.0)
+    rs = np.random.RandomState(5)
+    state = rs.randint(0, 256, size=(3, 84, 84, 4)).astype(np.uint8)
+    action = rs.randint(0, 4, size=3).astype(np.int64)
+    R = rs.normal(size=3).astype(np.float32)
+    m = TorchCpuBa3c(p32, 16, 2)
+    st, ac, rr = torch.from_numpy(state), torch.from_numpy(action), torch.from_numpy(R)
+    cost, g = m.loss_and_grads(st, ac, rr)
+    p64 = {k: v.astype(np.float64) for k, v in p32.items()}
+    _, sc, gref = O.loss_and_grads(p64, state, action, R.astype(np.float64), cfg)
+    assert abs(float(cost) - sc["cost"]) < 1e-5 * max(1.0, abs(sc["cost"]))
+    for k in gref:
+        err = np.abs(g[k].numpy() - gref[k]).max() / max(np.abs(gref[k]).max(), 1e-30)
+        assert err < 1e-4, (k, err)
+    m.step(st, ac, rr)
+    newp, _, _, gc = O.train_step(p64, O.init_slots(p64, "adam", 0.8, 0.75), 1,
+                                  [(state, action, R.astype(np.float64))], cfg)
+    for k in newp:
+        d_got = m.p[k].numpy().astype(np.float64) - p32[k]
+        d_ref = newp[k] - p64[k]
+        mask = np.abs(gc[k]) > 1e-4 * max(np.abs(gc[k]).max(), 1e-30)
+        if mask.any():
+            e = np.abs(d_got[mask] - d_ref[mask]).max() / np.abs(d_ref[mask]).max()
+            assert e < 1e-4, (k, e)
