@@ -29,9 +29,10 @@ namespace ba3c {
 // With KPH < CIN the band is staged in CIN/KPH channel phases through the same LDS (smaller
 // footprint => more workgroups per CU to hide the staging); accumulators persist across
 // phases, so a phased layout needs all of a wave's m-blocks in one chunk.
-template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0>
+template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0, int NS_ = 3>
 struct Band6 {
   using G = G_;
+  static constexpr int NS = NS_;                         // split planes (3 bf16 / 2 fp16)
   static constexpr int KPH = KPH_ ? KPH_ : G_::CIN;
   static constexpr int NPH = G_::CIN / KPH;
   static constexpr int PP = PP_, RP = G::WS * PP_ + RPX_, MCH = MCH_;
@@ -41,7 +42,7 @@ struct Band6 {
   static constexpr int NT = G::KH * G::KW * K32;         // k-steps per phase
   static constexpr int NCH = (G::MBW + MCH - 1) / MCH;   // m-block chunks per wave
   static_assert(KPH % 32 == 0 && G::CIN % KPH == 0 && PP % 16 == 0 && RP % 16 == 0 &&
-                PP >= 3 * SPB, "band6 layout");
+                PP >= NS * SPB, "band6 layout");
   static_assert(NPH == 1 || NCH == 1, "phased staging keeps every accumulator live");
   static_assert(LDS_BYTES <= 160 * 1024, "band6 LDS");
 };
@@ -49,11 +50,16 @@ struct Band6 {
 struct Band6Args {
   const float* src;        // SRC 0: input map [B,HS,WS,CIN];  SRC 1: dP [B,UPH,UPW,CIN]
   const uint8_t* code;     // SRC 1: argmax codes of dP
-  const uint16_t* wt6;     // [3][COUT][KH*KW*CIN] bf16 splits (prepared per step)
+  const uint16_t* wt6;     // [NS][COUT][KH*KW*CIN] 16-bit splits (prepared per step)
   float* out;              // POOL: pooled [B,HO/2,WO/2,COUT]; else [B,HO,WO,COUT]
   uint8_t* out_code;       // POOL: argmax codes (may be null: predictor)
   unsigned long long* relu_count;
   int batch;
+  // NS = 2 (scaled fp16): max |src| slots of the staged map (per image at [1 + img]), the
+  // weight scale exponent, and the slots that receive max |out| (may be null)
+  const uint32_t* amax_in;
+  const int* wexp;
+  uint32_t* amax_out;
 };
 
 template <class L>
@@ -72,6 +78,9 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
   // three bf16 planes ----
   // Index math is 32-bit from per-workgroup base pointers (the band of an SRC 0 map is one
   // contiguous run of rows); unsigned division by the compile-time Q / WS is a mul-hi.
+  using SP = SplitP<L::NS>;
+  const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
+  const float asc = exp2i(ka);
   auto stage = [&](int ph) {
     constexpr unsigned Q = L::KPH / 4;                   // float4 per pixel and phase
     const int cb = ph * L::KPH;
@@ -117,14 +126,14 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == sb ? e[k] : 0.f;
           }
-          uint32_t h0, m0, l0, h1, m1, l1;
-          split3x2(e[0], e[1], h0, m0, l0);
-          split3x2(e[2], e[3], h1, m1, l1);
+          uint32_t s0[L::NS], s1[L::NS];
+          SP::split(e[0], e[1], asc, s0);
+          SP::split(e[2], e[3], asc, s1);
           // ry * RP + x * PP == pix * PP + ry * (RP - WS * PP)
           char* p = lds + pix * L::PP + ry * (L::RP - G::WS * L::PP) + cq * 8;
-          *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
-          *reinterpret_cast<uint2*>(p + L::SPB) = make_uint2(m0, m1);
-          *reinterpret_cast<uint2*>(p + 2 * L::SPB) = make_uint2(l0, l1);
+#pragma unroll
+          for (int sp = 0; sp < L::NS; ++sp)
+            *reinterpret_cast<uint2*>(p + sp * L::SPB) = make_uint2(s0[sp], s1[sp]);
         }
       }
     }
@@ -138,12 +147,14 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
   const int mb0 = wave / G::NB;
   const int li = lane & 15, lq = lane >> 4;
   const int col = nb * 16 + li;
-  // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] bf16
+  // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] 16-bit
   const uint16_t* wrow = a.wt6 + (size_t)col * G::KDIM + 8 * lq;
   constexpr size_t WSPLIT = (size_t)G::COUT * G::KDIM;
   // K index (tap, channel) of k-step t of a phase, relative to the phase's first channel
   auto koff = [](int t) { return (t / L::K32) * G::CIN + (t % L::K32) * 32; };
   unsigned long long pos = 0;
+  const float us1 = exp2i(-ka), us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
+  float omax = 0.f;
 
 #pragma unroll
   for (int chn = 0; chn < L::NCH; ++chn) {
@@ -181,52 +192,46 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
     }
     const uint16_t* wph = wrow + ph * L::KPH;
     constexpr int LA = 2;
-    uint4 bring[LA + 1][3];
+    uint4 bring[LA + 1][L::NS];
 #pragma unroll
     for (int t = 0; t < LA && t < L::NT; ++t)
 #pragma unroll
-      for (int s = 0; s < 3; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
+      for (int s = 0; s < L::NS; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
 #pragma unroll
     for (int t = 0; t < L::NT; ++t) {
       if (t + LA < L::NT) {
 #pragma unroll
-        for (int s = 0; s < 3; ++s)
+        for (int s = 0; s < L::NS; ++s)
           bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t + LA));
       }
-      bf16x8 b[3];
+      u32x4 b[L::NS];
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
+      for (int s = 0; s < L::NS; ++s) {
         const uint4 u = bring[t % (LA + 1)][s];
-        b[s] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+        b[s] = u32x4{u.x, u.y, u.z, u.w};
       }
       const int tap = t / L::K32, ch = t - tap * L::K32;
       const int kh = tap / G::KW, kw = tap - kh * G::KW;
       const int toff = kh * L::RP + kw * L::PP + ch * 64;
-      bf16x8 av[3][MCH];
+      u32x4 av[L::NS][MCH];
 #pragma unroll
       for (int j = 0; j < MCH; ++j)
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
+        for (int s = 0; s < L::NS; ++s) {
           const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * L::SPB);
-          av[s][j] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+          av[s][j] = u32x4{u.x, u.y, u.z, u.w};
         }
-      // a1b1, a1b2, a2b1, a1b3, a2b2, a3b1 — interleaved over m-blocks
+      // NS = 3: a1b1, a1b2, a2b1, a1b3, a2b2, a3b1;  NS = 2: a1b1, a1b2, a2b1 —
+      // interleaved over m-blocks
 #pragma unroll
-      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][j], b[0], acc[j], 0, 0, 0);
+      for (int pr = 0; pr < SP::NPROD; ++pr)
 #pragma unroll
-      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][j], b[1], acc[j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][j], b[0], acc[j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][j], b[2], acc[j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][j], b[1], acc[j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < MCH; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][j], b[0], acc[j], 0, 0, 0);
+        for (int j = 0; j < MCH; ++j) acc[j] = SP::mfma(av[SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
     }
     }
 
     // ---- epilogue (16x16 C layout: lane holds column li, rows 4 lq + r) ----
+    // un-scale by 2^-(ka + kw) (two exact power-of-two products)
 #pragma unroll
     for (int j = 0; j < MCH; ++j) {
       const int mb = mb0 + (chn * MCH + j) * G::WPN;
@@ -243,7 +248,9 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
           if (v2 > mx) { mx = v2; arg = 2; }
           if (v3 > mx) { mx = v3; arg = 3; }
           const size_t o = ((size_t)(img * (G::HO / 2) + y0 / 2 + ph) * (G::WO / 2) + pw) * G::COUT + col;
-          a.out[o] = fmaxf(mx, 0.f);
+          const float out = fmaxf(mx, 0.f) * us1 * us2;
+          omax = fmaxf(omax, out);
+          a.out[o] = out;
           if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
         }
       } else {
@@ -251,43 +258,88 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
         for (int r = 0; r < 4; ++r) {
           const int row = mb * 16 + lq * 4 + r;
           const int oy = row / G::WO, ox = row - oy * G::WO;
-          if (row < G::MROWS && oy < rows_out)
-            a.out[((size_t)(img * G::HO + y0 + oy) * G::WO + ox) * G::COUT + col] = acc[j][r];
+          if (row < G::MROWS && oy < rows_out) {
+            const float out = acc[j][r] * us1 * us2;
+            omax = fmaxf(omax, fabsf(out));
+            a.out[((size_t)(img * G::HO + y0 + oy) * G::WO + ox) * G::COUT + col] = out;
+          }
         }
       }
     }
   }
   if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
+  if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
 }
 
 // One launch per step for all weight preparation on the split path: job y < njobs writes the
-// bf16 splits of band-conv copy y straight from the parameters (no fp32 [N][K] copy and no
-// second pass), job y == njobs (when w0 is set) prepares conv0's MFMA B fragments.
+// NS split planes of band-conv copy y straight from the parameters (no fp32 [N][K] copy and no
+// second pass), job y == njobs (when w0 is set) prepares conv0's MFMA B fragments.  With the
+// scaled fp16 family every workgroup of a job first reduces max |W| over the whole tensor
+// (L2-resident, <= 200 KB) and splits W * 2^kw; workgroup 0 publishes kw.  The same launch
+// zeroes the step's ReLU counters and max-|x| slots (nothing reads them before it ends).
 struct WPrep6Args {
   WPrepArgs jobs;
   uint16_t* wt6;
-  int off[4];              // fp32 offset of job i; its splits start at 3 * off[i]
+  int off[4];              // fp32 offset of job i; its splits start at NS * off[i]
   const float* w0;         // conv0/W (null: no conv0 job)
   uint4* wb0;
   unsigned long long* relu;  // training: ReLU-count slots zeroed here (no separate memset)
+  uint32_t* amax;          // max-|x| slots zeroed here (n_amax words; may be null)
+  int n_amax;
+  int* wexp;               // [5]: weight scale exponents of jobs 0..3 and conv0 (NS = 2)
 };
 
+template <int NS>
 __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
   const int y = blockIdx.y;
-  if (y == 0 && a.relu)
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < RELU_SLOTS; i += gridDim.x * 256) a.relu[i] = 0ull;
+  __shared__ float red4[4];
+  if (y == 0) {
+    if (a.relu)
+      for (int i = blockIdx.x * 256 + threadIdx.x; i < RELU_SLOTS; i += gridDim.x * 256) a.relu[i] = 0ull;
+    if (a.amax)
+      for (int i = blockIdx.x * 256 + threadIdx.x; i < a.n_amax; i += gridDim.x * 256) a.amax[i] = 0u;
+  }
   if (y == a.jobs.njobs) {
-    conv0s_wprep_one(a.w0, a.wb0, blockIdx.x * 256 + threadIdx.x);
+    int k = 0;
+    if constexpr (NS == 2) {
+      k = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, red4)));
+      if (blockIdx.x == 0 && threadIdx.x == 0) a.wexp[4] = k;
+    }
+    conv0s_wprep_one<NS>(a.w0, a.wb0, blockIdx.x * 256 + threadIdx.x, k);
     return;
   }
   const WPrepJob& j = a.jobs.job[y];
-  uint16_t* dst = a.wt6 + 3 * (size_t)a.off[y];
+  float sc = 1.f;
+  if constexpr (NS == 2) {
+    float m = 0.f;
+    const float4* w4 = reinterpret_cast<const float4*>(j.w);
+    for (int i = threadIdx.x; i < j.n / 4; i += 256) {
+      const float4 v = w4[i];
+      m = fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+    __syncthreads();
+    const int k = amax_exp(__float_as_uint(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]))));
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.wexp[y] = k;
+    sc = exp2i(k);
+  }
+  uint16_t* dst = a.wt6 + NS * (size_t)a.off[y];
   for (int e = blockIdx.x * 256 + threadIdx.x; e < j.n; e += gridDim.x * 256) {
-    uint32_t hi, mid, lo;
-    split3(wprep_value(j, e), hi, mid, lo);
-    dst[e] = (uint16_t)hi;
-    dst[j.n + e] = (uint16_t)mid;
-    dst[2 * j.n + e] = (uint16_t)lo;
+    const float v = wprep_value(j, e);
+    if constexpr (NS == 3) {
+      uint32_t hi, mid, lo;
+      split3(v, hi, mid, lo);
+      dst[e] = (uint16_t)hi;
+      dst[j.n + e] = (uint16_t)mid;
+      dst[2 * j.n + e] = (uint16_t)lo;
+    } else {
+      uint32_t hi, lo;
+      split2(v * sc, hi, lo);
+      dst[e] = (uint16_t)hi;
+      dst[j.n + e] = (uint16_t)lo;
+    }
   }
 }
 

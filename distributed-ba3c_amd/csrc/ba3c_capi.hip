@@ -71,6 +71,11 @@ struct ba3c_handle {
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  // split family of the split kernels: 2 = scaled fp16 hi/lo, 3 MFMAs per fp32 product
+  // (default); 3 = bf16 hi/mid/lo, 6 MFMAs (BA3C_SPLIT=bf16).  The fp16 family needs every
+  // producer of a split operand to publish its max, so it is used only when all split
+  // kernels are on (band, b6, w6, split).
+  int ns = 2;
   // backward weight gradients on a side stream (BA3C_OVERLAP=1; created on the first training
   // call that is not being captured). Off by default: r01t/u measured +0.5% step throughput
   // (561k vs 557k samples/s) because conv1's dgrad and wgrad kernels each fill the chip, and
@@ -95,29 +100,50 @@ using GConv1F = BandGeom<40, 40, 32, 32, 5, 5, 6, true, 0, 4>;
 using GConv2F = BandGeom<18, 18, 32, 64, 5, 5, 14, true, 0, 4>;
 using GConv1D = BandGeom<44, 44, 32, 32, 5, 5, 4, false, 1, 8, 4, 4, 18, 18, 36, 36>;
 using GConv2D = BandGeom<22, 22, 64, 32, 5, 5, 6, false, 1, 8, 4, 4, 7, 7, 14, 14>;
-// bf16x6 variants (ba3c_band6.h): pixel pitch / extra row bytes from a bank-conflict search
-using L6Conv1F = Band6<GConv1F, 192, 32, 7>;
-using L6Conv2F = Band6<GConv2F, 192, 32, 7>;
-using L6Conv1D = Band6<GConv1D, 224, 128, 5>;
-// conv2 input gradient: the whole 18x18 map per workgroup in two 32-channel phases (r01r:
-// 0.44 ms at 6-row bands -> 0.31 ms: no halo re-staging, 11 m-blocks per wave hide the
-// weight-fragment latency; 6 and 9-row bands and 8-row conv1 / 12-row conv1-fwd bands measured slower)
-using L6Conv2D = Band6<BandGeom<22, 22, 64, 32, 5, 5, 18, false, 1, 8, 4, 4, 7, 7, 14, 14>, 224, 128, 11, 32>;
-// small batches (B <= SMALL_B, e.g. configs[1]'s B=32): conv2 forward / input gradient in
-// 2- / 3-row bands, so the launch has 7x / 6x the workgroups of the whole-map kernels — at
-// B=32 those are 32 workgroups on 256 CUs, one latency-bound wave of work.  Every output's
-// K order (phase, tap, channel chunk, product) is the same in both geometries, so results
-// are bit-identical across the switch.
+// split-family variants (ba3c_band6.h): pixel pitch / extra row bytes from a bank-conflict
+// search (scripts/lds_bank_search.py), per family (3 bf16 planes or 2 fp16 planes per pixel)
+//  C2D: conv2 input gradient, the whole 18x18 map per workgroup in two 32-channel phases
+//       (r01r: 0.44 ms at 6-row bands -> 0.31 ms: no halo re-staging, 11 m-blocks per wave
+//       hide the weight-fragment latency; 6 and 9-row bands and 8-row conv1 / 12-row
+//       conv1-fwd bands measured slower)
+//  C2FS / C2DS: small batches (B <= SMALL_B, e.g. configs[1]'s B=32): conv2 forward / input
+//       gradient in 2- / 3-row bands, so the launch has 7x / 6x the workgroups of the
+//       whole-map kernels — at B=32 those are 32 workgroups on 256 CUs, one latency-bound
+//       wave of work.  Every output's K order (phase, tap, channel chunk, product) is the same
+//       in both geometries, so results are bit-identical across the switch.
 constexpr int SMALL_B = 128;
-using L6Conv2FS = Band6<BandGeom<18, 18, 32, 64, 5, 5, 2, true, 0, 4>, 192, 32, 2>;
-using L6Conv2DS = Band6<BandGeom<22, 22, 64, 32, 5, 5, 3, false, 1, 8, 4, 4, 7, 7, 14, 14>, 224, 128, 2, 32>;
+using GConv2DW = BandGeom<22, 22, 64, 32, 5, 5, 18, false, 1, 8, 4, 4, 7, 7, 14, 14>;
+using GConv2FS = BandGeom<18, 18, 32, 64, 5, 5, 2, true, 0, 4>;
+using GConv2DS = BandGeom<22, 22, 64, 32, 5, 5, 3, false, 1, 8, 4, 4, 7, 7, 14, 14>;
+template <int NS>
+struct Lay;
+template <>
+struct Lay<3> {
+  using C1F = Band6<GConv1F, 192, 32, 7, 0, 3>;
+  using C2F = Band6<GConv2F, 192, 32, 7, 0, 3>;
+  using C1D = Band6<GConv1D, 224, 128, 5, 0, 3>;
+  using C2D = Band6<GConv2DW, 224, 128, 11, 32, 3>;
+  using C2FS = Band6<GConv2FS, 192, 32, 2, 0, 3>;
+  using C2DS = Band6<GConv2DS, 224, 128, 2, 32, 3>;
+  using W1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 224, 3>;
+  using W2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 192, 3>;
+};
+template <>
+struct Lay<2> {
+  using C1F = Band6<GConv1F, 160, 128, 7, 0, 2>;
+  using C2F = Band6<GConv2F, 160, 64, 7, 0, 2>;
+  using C1D = Band6<GConv1D, 160, 128, 5, 0, 2>;
+  using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2>;
+  using C2FS = Band6<GConv2FS, 160, 64, 2, 0, 2>;
+  using C2DS = Band6<GConv2DS, 160, 128, 2, 32, 2>;
+  using W1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 160, 2>;
+  using W2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 160, 2>;
+};
 // weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
 using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
 using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
 using GWg2 = WgGeom<18, 18, 32, 5, 5, 64, 7, false, 2>;
 constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
-using G6Wg1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 224>;
-using G6Wg2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 192>;
 constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workgroups
 constexpr int FW_P0S = 512;   // conv0s_fwd_kernel: persistent, two workgroups per CU
 constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
@@ -131,8 +157,13 @@ struct Workspace {
   uint16_t* wt6;   // [3][N][K] bf16 splits of the four band-conv weight copies
   uint8_t *c0, *c1, *c2;
   unsigned long long* relu;
+  uint32_t* amax;  // [AMAX_N][1 + max_batch]: max |x| of split operands (global, per image)
+  int* wexp;       // [8]: weight scale exponents (wprep jobs 0..3, conv0 = 4)
   size_t bytes;
+  uint32_t* am(int t, const ba3c_handle* h) const { return amax + (size_t)t * (1 + h->cfg.max_batch); }
 };
+// max-|x| slot arrays (ba3c_split.h, fp16 family)
+enum { AM_P0 = 0, AM_P1 = 1, AM_DP0 = 2, AM_DP1 = 3, AM_DP2 = 4, AMAX_N = 5 };
 
 struct WgradPlan {
   int M, N, K, S, kchunk, mt, nt;
@@ -166,7 +197,7 @@ size_t max_partials0(const ba3c_handle* h, int B) {
   const WgradPlan w = plan_wgrad(25 * h->cfg.channels, 32, B * 6400, 128, 32);
   mx = std::max(mx, (size_t)w.S * w.M * w.N);
   mx = std::max(mx, (size_t)WG_P0 * GWg0::M * 32);
-  mx = std::max(mx, (size_t)WG_P0S * Conv0W::M * 32);
+  mx = std::max(mx, (size_t)WG_P0S * Conv0W<3>::M * 32);
   return mx;
 }
 
@@ -181,8 +212,8 @@ size_t max_partials(const ba3c_handle* h, int B) {
   upd(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
   mx = std::max(mx, (size_t)WG_P1 * GWg1::M * 32);
   mx = std::max(mx, (size_t)WG_P2 * GWg2::M * 64);
-  mx = std::max(mx, (size_t)W6_P1 * G6Wg1::M * G6Wg1::COUT);
-  mx = std::max(mx, (size_t)W6_P2 * G6Wg2::M * G6Wg2::COUT);
+  mx = std::max(mx, (size_t)W6_P1 * Lay<3>::W1::M * Lay<3>::W1::COUT);
+  mx = std::max(mx, (size_t)W6_P2 * Lay<3>::W2::M * Lay<3>::W2::COUT);
   return mx;
 }
 
@@ -201,6 +232,8 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   // The clip / optimizer per-chunk sum-of-squares partials come FIRST, at a batch-independent
   // offset: ba3c_clip_grads / ba3c_apply_update receive only the workspace base.
   w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
+  w.amax = (uint32_t*)take((size_t)AMAX_N * (1 + h->cfg.max_batch) * 4);
+  w.wexp = (int*)take(8 * 4);
   w.p0 = (float*)take(Bz * P0 * 4);
   w.p1 = (float*)take(Bz * P1 * 4);
   w.p2 = (float*)take(Bz * P2 * 4);
@@ -286,10 +319,17 @@ int launch_band(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a) {
   return BA3C_OK;
 }
 
+// Split operands of a band-conv launch (fp16 family): the max slots of the staged map, the
+// weight job whose scale exponent applies, and the slots that receive max |out| (-1: none).
+struct SplitIO {
+  int amax_in, wjob, amax_out;
+};
+
 template <class L>
 int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
-                 int wt_off) {
-  const Band6Args b{a.src, a.code, w.wt6 + 3 * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch};
+                 int wt_off, SplitIO io) {
+  const Band6Args b{a.src, a.code, w.wt6 + L::NS * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch,
+                    w.am(io.amax_in, h), w.wexp + io.wjob, io.amax_out >= 0 ? w.am(io.amax_out, h) : nullptr};
   dim3 grid(a.batch * L::G::NBANDS);
   {
     ProbeScope ps(h, s, kid);
@@ -299,11 +339,11 @@ int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, cons
   return BA3C_OK;
 }
 
-// band conv: bf16x6 split MFMA when enabled, fp32 MFMA otherwise
+// band conv: split MFMA when enabled, fp32 MFMA otherwise
 template <class L>
 int launch_bandx(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
-                 int wt_off) {
-  if (h->b6) return launch_band6<L>(h, s, kid, a, w, wt_off);
+                 int wt_off, SplitIO io) {
+  if (h->b6) return launch_band6<L>(h, s, kid, a, w, wt_off, io);
   return launch_band<typename L::G>(h, s, kid, a);
 }
 
@@ -328,7 +368,7 @@ int launch_wgband(ba3c_handle* h, hipStream_t s, int kid, const WgArgs& a, int p
   return launch_reduce(h, s, a.part, P, mp);
 }
 
-// bf16x6 weight-gradient kernel + deterministic reduction into the flat HWIO grads
+// split weight-gradient kernel + deterministic reduction into the flat HWIO grads
 template <class G>
 int launch_wgrad6(ba3c_handle* h, hipStream_t s, int kid, const Wg6Args& a, int pmax, float* dst) {
   const int P = std::min(pmax, a.batch * G::NBANDS);
@@ -348,6 +388,7 @@ int launch_wgrad6(ba3c_handle* h, hipStream_t s, int kid, const Wg6Args& a, int 
 }
 
 // [N][K] copies of the band-conv weights for this step (forward; + rotated dgrad in training)
+template <int NS>
 int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, bool train) {
   const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
   const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
@@ -359,7 +400,7 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
   a.njobs = train ? 4 : 2;
   const bool c0s = h->cfg.channels == 4 && h->split;
   if (h->b6) {
-    // split path: one launch writes the bf16 splits (and conv0's fragments) directly
+    // split path: one launch writes the splits (and conv0's fragments) directly
     WPrep6Args pa{};
     pa.jobs = a;
     pa.wt6 = w.wt6;
@@ -368,7 +409,10 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
     pa.w0 = c0s ? prm + h->tensors[h->idx_conv[0]].offset : nullptr;
     pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
     pa.relu = train ? w.relu : nullptr;
-    hipLaunchKernelGGL(wprep6_kernel, dim3(64, a.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
+    pa.amax = w.amax;
+    pa.n_amax = AMAX_N * (1 + h->cfg.max_batch);
+    pa.wexp = w.wexp;
+    hipLaunchKernelGGL(wprep6_kernel<NS>, dim3(64, a.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
     HIP_TRY(hipGetLastError());
   } else {
     hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
@@ -389,13 +433,15 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
   return BA3C_OK;
 }
 
-int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a) {
+template <int NS>
+int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a, const Workspace& w) {
   if (h->split) {
     const Conv0SArgs sa{reinterpret_cast<const uint8_t*>(a.src),
-                        reinterpret_cast<const uint4*>(a.wt - WT_C0F + WT_C0S), a.out, a.out_code,
-                        a.relu_count, a.batch};
+                        reinterpret_cast<const uint4*>(w.wt + WT_C0S), a.out, a.out_code,
+                        a.relu_count, a.batch, w.wexp + 4, w.am(AM_P0, h)};
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-    hipLaunchKernelGGL(conv0s_fwd_kernel, dim3(std::min(FW_P0S, a.batch * Conv0S::NBANDS)), dim3(256), 0, s, sa);
+    hipLaunchKernelGGL(conv0s_fwd_kernel<NS>, dim3(std::min(FW_P0S, a.batch * Conv0S::NBANDS)), dim3(256), 0,
+                       s, sa);
   } else {
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
     hipLaunchKernelGGL(conv0_band_kernel, dim3(a.batch * Conv0Geom::NBANDS), dim3(256), 0, s, a);
@@ -405,33 +451,38 @@ int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a) {
 }
 
 // ---- forward --------------------------------------------------------------------------
-template <int CH>
+// NS: split family of the split kernels (2 scaled fp16, 3 bf16); see ba3c_split.h.
+template <int CH, int NS>
 int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
                 const Workspace& w, bool train) {
+  using LY = Lay<NS>;
   const int F = h->cfg.fc_neurons;
   const float* W0 = prm + h->tensors[h->idx_conv[0]].offset;
   const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
   const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3 = prm + h->tensors[h->idx_conv[3]].offset;
   unsigned long long* rc = train ? w.relu : nullptr;
-  if (h->band) CHECK(launch_wprep(h, s, prm, w, train));
+  uint32_t* am_p0 = w.am(AM_P0, h);
+  const SplitIO io1{AM_P0, 0, AM_P1}, io2{AM_P1, 1, -1};
+  if (h->band) CHECK(launch_wprep<NS>(h, s, prm, w, train));
   if (train) {
     if (h->band && CH == 4) {
-      CHECK(launch_conv0_band(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
-                                             w.wt + WT_C0F, w.p0, w.c0, rc, B}));
+      CHECK(launch_conv0_band<NS>(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
+                                                 w.wt + WT_C0F, w.p0, w.c0, rc, B}, w));
     } else {
       ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> c0{state, W0, w.p0, w.c0, rc, 1.0f / 255.0f,
-                                                   B * 6400, 32, 25 * CH, 0};
+                                                   B * 6400, 32, 25 * CH, 0, am_p0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
     }
     if (h->band) {
-      CHECK(launch_bandx<L6Conv1F>(h, s, BA3C_K_CONV1_FWD,
-                                     BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}, w, WT_C1F));
+      CHECK(launch_bandx<typename LY::C1F>(h, s, BA3C_K_CONV1_FWD,
+                                          BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}, w,
+                                          WT_C1F, io1));
       const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B};
       if (h->b6 && B <= SMALL_B)
-        CHECK(launch_band6<L6Conv2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
+        CHECK(launch_band6<typename LY::C2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
       else
-        CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
+        CHECK(launch_bandx<typename LY::C2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
     } else {
       ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> c1{w.p0, W1, w.p1, w.c1, rc, 1.0f, B * 1296, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
@@ -440,20 +491,21 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
     }
   } else if (h->band) {
     if (CH == 4) {
-      CHECK(launch_conv0_band(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
-                                             w.wt + WT_C0F, w.p0, nullptr, nullptr, B}));
+      CHECK(launch_conv0_band<NS>(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
+                                                 w.wt + WT_C0F, w.p0, nullptr, nullptr, B}, w));
     } else {
       ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
-                                                   B * 6400, 32, 25 * CH, 0};
+                                                   B * 6400, 32, 25 * CH, 0, am_p0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
     }
-    CHECK(launch_bandx<L6Conv1F>(h, s, BA3C_K_CONV1_FWD,
-                                   BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}, w, WT_C1F));
+    CHECK(launch_bandx<typename LY::C1F>(h, s, BA3C_K_CONV1_FWD,
+                                        BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}, w,
+                                        WT_C1F, io1));
     const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B};
     if (h->b6 && B <= SMALL_B)
-      CHECK(launch_band6<L6Conv2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
+      CHECK(launch_band6<typename LY::C2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
     else
-      CHECK(launch_bandx<L6Conv2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F));
+      CHECK(launch_bandx<typename LY::C2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
   } else {
     ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
                                                  B * 6400, 32, 25 * CH, 0};
@@ -493,9 +545,10 @@ int ensure_side_stream(ba3c_handle* h, hipStream_t s) {
   return BA3C_OK;
 }
 
-template <int CH>
+template <int CH, int NS>
 int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
                  const Workspace& w, float* grads) {
+  using LY = Lay<NS>;
   const int F = h->cfg.fc_neurons, A = h->cfg.num_actions;
   const bool legacy = !h->cfg.replace_with_conv;
   const float* W1c = prm + h->tensors[h->idx_conv[1]].offset;
@@ -569,15 +622,16 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
     CHECK(conv_reduce(pl, 3, 64, 64));
-    ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0};
+    ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0, w.am(AM_DP2, h)};
     CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
     CHECK(fork());
   }
   // conv2
   {
     if (h->band && h->w6) {
-      CHECK(launch_wgrad6<G6Wg2>(h, ws, BA3C_K_CONV2_WGRAD, Wg6Args{w.p1, w.dp2, w.c2, w.part, B}, W6_P2,
-                                 grads + h->tensors[h->idx_conv[2]].offset));
+      CHECK(launch_wgrad6<typename LY::W2>(h, ws, BA3C_K_CONV2_WGRAD,
+                                          Wg6Args{w.p1, w.dp2, w.c2, w.part, B, w.am(AM_P1, h), w.am(AM_DP2, h)},
+                                          W6_P2, grads + h->tensors[h->idx_conv[2]].offset));
     } else if (h->band) {
       CHECK(launch_wgband<GWg2>(h, ws, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part, B}, WG_P2,
                                 grads + h->tensors[h->idx_conv[2]].offset, 32));
@@ -589,10 +643,11 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
     if (h->band) {
       const BandArgs ba{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B};
+      const SplitIO io{AM_DP2, 3, AM_DP1};
       if (h->b6 && B <= SMALL_B)
-        CHECK(launch_band6<L6Conv2DS>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D));
+        CHECK(launch_band6<typename LY::C2DS>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D, io));
       else
-        CHECK(launch_bandx<L6Conv2D>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D));
+        CHECK(launch_bandx<typename LY::C2D>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D, io));
     } else {
       ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
@@ -602,8 +657,9 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // conv1
   {
     if (h->band && h->w6) {
-      CHECK(launch_wgrad6<G6Wg1>(h, ws, BA3C_K_CONV1_WGRAD, Wg6Args{w.p0, w.dp1, w.c1, w.part, B}, W6_P1,
-                                 grads + h->tensors[h->idx_conv[1]].offset));
+      CHECK(launch_wgrad6<typename LY::W1>(h, ws, BA3C_K_CONV1_WGRAD,
+                                          Wg6Args{w.p0, w.dp1, w.c1, w.part, B, w.am(AM_P0, h), w.am(AM_DP1, h)},
+                                          W6_P1, grads + h->tensors[h->idx_conv[1]].offset));
     } else if (h->band) {
       CHECK(launch_wgband<GWg1>(h, ws, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part, B}, WG_P1,
                                 grads + h->tensors[h->idx_conv[1]].offset, 32));
@@ -615,7 +671,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
     if (h->band) {
       const BandArgs ba{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B};
-      CHECK(launch_bandx<L6Conv1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D));
+      CHECK(launch_bandx<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0}));
     } else {
       ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
@@ -623,16 +679,16 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   }
   // conv0 (no input gradient: the frames are not trainable)
   if (h->band && CH == 4 && h->split) {
-    const int P = std::min(WG_P0S, B * Conv0W::NBANDS);
+    const int P = std::min(WG_P0S, B * Conv0W<NS>::NBANDS);
     {
       ProbeScope ps(h, s, BA3C_K_CONV0_WGRAD);
-      hipLaunchKernelGGL(conv0s_wgrad_kernel, dim3(P), dim3(256), 0, s,
-                         Conv0WArgs{state, w.dp0, w.c0, w.part0, B});
+      hipLaunchKernelGGL(conv0s_wgrad_kernel<NS>, dim3(P), dim3(256), 0, s,
+                         Conv0WArgs{state, w.dp0, w.c0, w.part0, B, w.am(AM_DP0, h)});
     }
     HIP_TRY(hipGetLastError());
     ReduceMap mp{};
     mp.kind = 0;
-    mp.M = Conv0W::M;
+    mp.M = Conv0W<NS>::M;
     mp.N = 32;
     mp.cin = 4;
     mp.cinpad = 16;
@@ -724,6 +780,8 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = (e[0] == '1');
+  if (const char* e = getenv("BA3C_SPLIT")) h->ns = (std::strcmp(e, "bf16") == 0) ? 3 : 2;
+  if (!(h->band && h->b6 && h->w6 && h->split)) h->ns = 3;
 
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
@@ -853,8 +911,10 @@ int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
   Workspace w = carve(h, workspace, batch, false);
-  int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, false)
-                               : run_forward<12>(h, s, params, state, batch, w, false);
+  int r = h->cfg.channels == 4 ? (h->ns == 2 ? run_forward<4, 2>(h, s, params, state, batch, w, false)
+                                               : run_forward<4, 3>(h, s, params, state, batch, w, false))
+                               : (h->ns == 2 ? run_forward<12, 2>(h, s, params, state, batch, w, false)
+                                             : run_forward<12, 3>(h, s, params, state, batch, w, false));
   if (r != BA3C_OK) return r;
   return run_heads(h, s, params, w, batch, nullptr, nullptr, 0.f, explore_factor, false, probs,
                    probsT, value);
@@ -873,8 +933,10 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
   HIP_TRY(hipMemsetAsync(grads, 0, (size_t)h->flat * 4, s));
   // on the band + split path the weight-prep launch zeroes the ReLU counters
   if (!(h->band && h->b6)) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_SLOTS * 8, s));
-  int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, true)
-                               : run_forward<12>(h, s, params, state, batch, w, true);
+  int r = h->cfg.channels == 4 ? (h->ns == 2 ? run_forward<4, 2>(h, s, params, state, batch, w, true)
+                                               : run_forward<4, 3>(h, s, params, state, batch, w, true))
+                               : (h->ns == 2 ? run_forward<12, 2>(h, s, params, state, batch, w, true)
+                                             : run_forward<12, 3>(h, s, params, state, batch, w, true));
   if (r != BA3C_OK) return r;
   CHECK(run_heads(h, s, params, w, batch, action, futurereward, entropy_beta, 1.0f, true, nullptr,
                   nullptr, nullptr));
@@ -883,8 +945,11 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
                        w.relu, scalars);
     HIP_TRY(hipGetLastError());
   }
-  return h->cfg.channels == 4 ? run_backward<4>(h, s, params, state, batch, w, grads)
-                              : run_backward<12>(h, s, params, state, batch, w, grads);
+  if (h->cfg.channels == 4)
+    return h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads)
+                      : run_backward<4, 3>(h, s, params, state, batch, w, grads);
+  return h->ns == 2 ? run_backward<12, 2>(h, s, params, state, batch, w, grads)
+                    : run_backward<12, 3>(h, s, params, state, batch, w, grads);
 }
 
 int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace) {
@@ -1069,13 +1134,13 @@ int ba3c_kernel_split(const ba3c_handle* h, int32_t kid) {
   const bool c4 = h->cfg.channels == 4;
   switch (kid) {
     case BA3C_K_CONV0_FWD:
-    case BA3C_K_CONV0_WGRAD: return (h->band && c4 && h->split) ? 3 : 1;
+    case BA3C_K_CONV0_WGRAD: return (h->band && c4 && h->split) ? h->ns : 1;
     case BA3C_K_CONV1_FWD:
     case BA3C_K_CONV2_FWD:
     case BA3C_K_CONV1_DGRAD:
-    case BA3C_K_CONV2_DGRAD: return (h->band && h->b6) ? 6 : 1;
+    case BA3C_K_CONV2_DGRAD: return (h->band && h->b6) ? (h->ns == 2 ? 3 : 6) : 1;
     case BA3C_K_CONV1_WGRAD:
-    case BA3C_K_CONV2_WGRAD: return (h->band && h->w6) ? 6 : 1;
+    case BA3C_K_CONV2_WGRAD: return (h->band && h->w6) ? (h->ns == 2 ? 3 : 6) : 1;
     case BA3C_K_HEADS:
     case BA3C_K_WGRAD_REDUCE:
     case BA3C_K_CLIP:

@@ -42,6 +42,20 @@ __device__ __forceinline__ void relu_count_add_uniform(unsigned long long* slots
   }
 }
 
+// Max |x| of a tensor, published for the scaled-fp16 split kernels that consume it
+// (ba3c_split.h): lane 0 of a wave adds the wave's max of image img to slot [1 + img] and to
+// the global slot [0] (atomicMax on the bits of a non-negative float orders like the float).
+// Every lane of the wave must call it (wave-wide reduction).
+__device__ __forceinline__ void amax_publish(uint32_t* slots, int img, float m, int lane) {
+  if (!slots) return;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0 && m > 0.f) {
+    atomicMax(slots + 1 + img, __float_as_uint(m));
+    atomicMax(slots, __float_as_uint(m));
+  }
+}
+
 // dY at conv-output position (y, x) from pooled grad dP and argmax codes.
 template <int PW, int COUT>
 __device__ __forceinline__ float4 unpool4(const float* __restrict__ dP, const uint8_t* __restrict__ code,
@@ -79,6 +93,7 @@ struct ConvFwd {
   unsigned long long* relu_count;
   float scale;
   int M, N, K, kchunk;
+  uint32_t* amax;        // MODE 0/1: max of the pooled output per image (may be null)
 
   __device__ int a_row(int m) const {
     if (m >= M) return -1;
@@ -121,6 +136,10 @@ struct ConvFwd {
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
     const int j = lane & 31, h = lane >> 5;
     unsigned long long pos = 0;
+    constexpr int WPI = MODE != 2 ? PH * PW : 1;       // pooling windows per image
+    static_assert(MODE == 2 || TM * 8 <= WPI, "a wave's windows span at most two images");
+    const int n0 = (mrow >> 2) / WPI;
+    float m0 = 0.f, m1 = 0.f;   // max pooled output of images n0, n0 + 1 in this lane's rows
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -140,7 +159,10 @@ struct ConvFwd {
             if (v3 > mx) { mx = v3; arg = 3; }
             const int win = wbase + 2 * q + h;
             if (win * 4 < M && col < N) {
-              out[(size_t)win * COUT + col] = fmaxf(mx, 0.f);
+              const float o = fmaxf(mx, 0.f);
+              out[(size_t)win * COUT + col] = o;
+              if (win / WPI == n0) m0 = fmaxf(m0, o);
+              else m1 = fmaxf(m1, o);
               if constexpr (MODE == 0) code[(size_t)win * COUT + col] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
             }
           }
@@ -155,6 +177,10 @@ struct ConvFwd {
         }
       }
     if (relu_count) relu_count_add(relu_count, pos, lane);
+    if (MODE != 2 && amax) {
+      amax_publish(amax, n0, m0, lane);
+      if (((mrow + TM * 32 - 1) >> 2) / WPI > n0) amax_publish(amax, n0 + 1, m1, lane);
+    }
   }
 };
 
@@ -174,6 +200,7 @@ struct ConvDgrad {
   const float* w;        // [KH,KW,CIN,COUT]
   float* dx;             // [B,HIN,WIN,CIN]
   int M, N, K, kchunk;
+  uint32_t* amax;        // max |dx| per image (amax_publish slots; may be null)
 
   __device__ ARow a_row(int m) const {
     ARow r;
@@ -206,7 +233,10 @@ struct ConvDgrad {
   }
   template <int TM, int TN>
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
+    static_assert(TM * 32 <= HIN * WIN, "a wave's rows span at most two images");
     const int j = lane & 31;
+    const int n0 = mrow / (HIN * WIN);
+    float m0 = 0.f, m1 = 0.f;   // max |dx| of images n0 and n0 + 1 in this lane's rows
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -215,9 +245,18 @@ struct ConvDgrad {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = mrow + a * 32 + acc_row(r, lane);
-          if (m < M && col < N) dx[(size_t)m * CIN + col] = acc[a][b][r];
+          if (m < M && col < N) {
+            const float v = acc[a][b][r];
+            dx[(size_t)m * CIN + col] = v;
+            if (m / (HIN * WIN) == n0) m0 = fmaxf(m0, fabsf(v));
+            else m1 = fmaxf(m1, fabsf(v));
+          }
         }
       }
+    if (amax) {
+      amax_publish(amax, n0, m0, lane);
+      if ((mrow + TM * 32 - 1) / (HIN * WIN) > n0) amax_publish(amax, n0 + 1, m1, lane);
+    }
   }
 };
 

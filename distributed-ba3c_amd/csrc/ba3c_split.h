@@ -64,36 +64,133 @@ __device__ __forceinline__ void split3x2(float a, float b, uint32_t& hi, uint32_
   lo = pack_bf16x2(sa, sb);
 }
 
+// ---------------------------------------------------------------------------------------
+// The second split family (default): fp16 hi + lo of a power-of-two-scaled value.
+//
+// x * 2^k = hi + lo + r with hi = RN_f16(x 2^k), lo = RN_f16(x 2^k - hi) (the difference is
+// exact in fp32: Sterbenz), |r| <= 2^-22 |x 2^k|: 22 significant bits in two fp16 numbers.
+// a*b = a1b1 + a1b2 + a2b1 + O(3 * 2^-22 |a||b|), every product exact in fp32, accumulated in
+// fp32 by v_mfma_f32_16x16x32_f16: THREE MFMAs per fp32 product (vs six for bf16 hi/mid/lo).
+// fp16's exponent range is narrow, so every operand tensor is scaled by 2^k chosen from its
+// max |x| (amax_exp: max * 2^k in [2^14, 2^15)); the scale is exact and the accumulator is
+// multiplied by 2^-(ka + kb) in the epilogue.  The activation / gradient maps are scaled PER
+// IMAGE (the results of an image do not depend on the batch it runs in), weights per tensor,
+// and the weight-gradient kernels use the whole tensor's max.  Producers publish the maxima
+// (amax_publish) into per-image slots [1 + img] and a global slot [0].
+// ---------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+// RNE fp32 pair -> packed fp16 pair (v_cvt_pk_f16_f32)
+__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, f16x2v));
+}
+// (a, b) = hi + lo (+ 2^-22 relative), each a packed fp16 pair
+__device__ __forceinline__ void split2x2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pack_f16x2(a, b);
+  const f16x2v h = __builtin_bit_cast(f16x2v, hi);
+  lo = pack_f16x2(a - (float)h[0], b - (float)h[1]);
+}
+__device__ __forceinline__ void split2(float w, uint32_t& hi, uint32_t& lo) {
+  uint32_t h2, l2;
+  split2x2(w, 0.f, h2, l2);
+  hi = h2 & 0xFFFFu;
+  lo = l2 & 0xFFFFu;
+}
+
+// exponent k with amax * 2^k in [2^14, 2^15) (0 for an all-zero tensor), clamped
+__device__ __forceinline__ int amax_exp(uint32_t amax_bits) {
+  if (amax_bits == 0u) return 0;
+  const int e = (int)((amax_bits >> 23) & 255u) - 127;   // floor(log2(amax)), normal amax
+  return max(-100, min(100, 14 - e));
+}
+__device__ __forceinline__ float exp2i(int k) { return __int_as_float((k + 127) << 23); }
+
+// split-family policy: NS planes per operand and the cross products that are kept
+template <int NS>
+struct SplitP;
+template <>
+struct SplitP<3> {   // bf16 hi/mid/lo: a1b1, a1b2, a2b1, a1b3, a2b2, a3b1
+  static constexpr int NPROD = 6;
+  __device__ static constexpr int pa(int p) { return p == 2 || p == 4 ? 1 : (p == 5 ? 2 : 0); }
+  __device__ static constexpr int pb(int p) { return p == 1 || p == 4 ? 1 : (p == 3 ? 2 : 0); }
+  __device__ static __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+  // two values -> NS packed planes (no scaling: bf16 has fp32's exponent range)
+  __device__ static __forceinline__ void split(float a, float b, float, uint32_t (&o)[3]) {
+    split3x2(a, b, o[0], o[1], o[2]);
+  }
+};
+template <>
+struct SplitP<2> {   // scaled fp16 hi/lo: a1b1, a1b2, a2b1
+  static constexpr int NPROD = 3;
+  __device__ static constexpr int pa(int p) { return p == 2 ? 1 : 0; }
+  __device__ static constexpr int pb(int p) { return p == 1 ? 1 : 0; }
+  __device__ static __forceinline__ f32x4 mfma(const u32x4& a, const u32x4& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+  __device__ static __forceinline__ void split(float a, float b, float scale, uint32_t (&o)[2]) {
+    split2x2(a * scale, b * scale, o[0], o[1]);
+  }
+};
+
 struct Conv0S {
   static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
   static constexpr int HO = 80, WO = 80, RB = 16, NBANDS = HO / RB, SROWS = RB + KT - 1;
   static constexpr int KSTEPS = 4;                 // 4 x 32 K = 32 tap slots (25 used)
-  static constexpr int NSPLIT = 3;
+  static constexpr int MAXSPLIT = 3;
   static constexpr int PROWS_W = RB / 2 / 4;       // pooled rows per wave (2)
   static constexpr int MBROW = (WO / 2) / 4;       // m-blocks per pooled row (10)
   static constexpr int MBW = PROWS_W * MBROW;      // m-blocks per wave (20)
   static constexpr int MCH = 5;                    // m-blocks per accumulator chunk
-  // prepared weights: [split][nt][kstep][lane] x 16 bytes
-  static constexpr int WB_U4 = NSPLIT * 2 * KSTEPS * 64;
+  // prepared weights: [split][nt][kstep][lane] x 16 bytes (room for the 3-plane family)
+  static constexpr int WB_U4 = MAXSPLIT * 2 * KSTEPS * 64;
   static_assert(RB % 8 == 0 && HO % RB == 0 && MBW % MCH == 0, "conv0 split geometry");
 };
 
-// conv0/W [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99; real channels c < 4) -> bf16 splits
-// in MFMA B-fragment order.  One thread per (nt, kstep, lane).
-__device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, uint4* __restrict__ wb, int t) {
+// real-channel weight of conv0/W [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99) at
+// K position (kstep s, lane group q, element e) = tap 8s + 2q + (e >> 2), channel e & 3
+__device__ __forceinline__ float conv0_w(const float* __restrict__ w, int s, int q, int e, int n) {
+  const int tap = 8 * s + 2 * q + (e >> 2), c = e & 3;
+  return tap < Conv0S::NTAP ? w[((size_t)tap * 16 + c) * 32 + n] : 0.f;
+}
+
+// max |w| over conv0's real-channel weights, reduced over the calling workgroup (256 threads)
+__device__ __forceinline__ float conv0_wmax_block(const float* __restrict__ w, float* red4) {
+  float m = 0.f;
+  for (int i = threadIdx.x; i < Conv0S::NTAP * 4 * 32; i += 256) {
+    const int tap = i / 128, c = (i >> 5) & 3, n = i & 31;
+    m = fmaxf(m, fabsf(w[((size_t)tap * 16 + c) * 32 + n]));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+  __syncthreads();
+  return fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
+}
+
+// conv0 weights -> NS split planes in MFMA B-fragment order (NS = 2: scaled by 2^kexp).
+// One thread per (nt, kstep, lane).
+template <int NS>
+__device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, uint4* __restrict__ wb, int t,
+                                                 int kexp) {
   using G = Conv0S;
   if (t >= 2 * G::KSTEPS * 64) return;
   const int lane = t & 63, s = (t >> 6) % G::KSTEPS, nt = t / (64 * G::KSTEPS);
   const int n = nt * 16 + (lane & 15), q = lane >> 4;
-  uint32_t part[3][8];
+  const float sc = exp2i(kexp);
+  uint32_t part[NS][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int tap = 8 * s + 2 * q + (e >> 2), c = e & 3;
-    const float v = tap < G::NTAP ? w[((size_t)tap * 16 + c) * 32 + n] : 0.f;
-    split3(v, part[0][e], part[1][e], part[2][e]);
+    const float v = conv0_w(w, s, q, e, n);
+    if constexpr (NS == 3) split3(v, part[0][e], part[1][e], part[2][e]);
+    else split2(v * sc, part[0][e], part[1][e]);
   }
 #pragma unroll
-  for (int sp = 0; sp < 3; ++sp)
+  for (int sp = 0; sp < NS; ++sp)
     wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane] =
         make_uint4(part[sp][0] | (part[sp][1] << 16), part[sp][2] | (part[sp][3] << 16),
                    part[sp][4] | (part[sp][5] << 16), part[sp][6] | (part[sp][7] << 16));
@@ -101,7 +198,7 @@ __device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, ui
 
 __global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restrict__ w,
                                                            uint4* __restrict__ wb) {
-  conv0s_wprep_one(w, wb, blockIdx.x * 256 + threadIdx.x);
+  conv0s_wprep_one<3>(w, wb, blockIdx.x * 256 + threadIdx.x, 0);
 }
 
 // Persistent workgroups walk bands (one image x RB output rows = RB/2 pooled rows); wave w
@@ -109,19 +206,31 @@ __global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restri
 // The weight splits are loaded into registers once per workgroup, and the next band's frame
 // rows are loaded into registers before the current band's MFMAs, so HBM latency hides
 // behind the arithmetic.  M rows are ordered (window, sub) so a lane's 4 accumulator rows
-// are one 2x2 window.
+// are one 2x2 window.  Frame bytes are exact in bf16 and in fp16 alike (no scaling); the
+// weights carry 2^kw (NS = 2), removed with the 1/255 in the epilogue.
 struct Conv0SArgs {
   const uint8_t* x;        // frames [B,84,84,4]
-  const uint4* wb;         // prepared bf16 weight splits
+  const uint4* wb;         // prepared weight splits
   float* out;              // pooled [B,40,40,32]
   uint8_t* out_code;       // argmax codes (may be null)
   unsigned long long* relu_count;
   int batch;
+  const int* wexp;         // NS = 2: exponent of the weight scale
+  uint32_t* amax_out;      // NS = 2: per-image max of the pooled output (may be null)
 };
 
+// a frame byte pair -> packed 16-bit pair of the split family
+template <int NS>
+__device__ __forceinline__ uint32_t u8pair(uint32_t a, uint32_t b) {
+  if constexpr (NS == 3) return u8_bf16(a) | (u8_bf16(b) << 16);
+  else return pack_f16x2((float)a, (float)b);
+}
+
+template <int NS>
 __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
   using G = Conv0S;
-  __shared__ uint2 xs[G::SROWS * G::WS];            // bf16 pixels (4 channels), 13.4 KB
+  using SP = SplitP<NS>;
+  __shared__ uint2 xs[G::SROWS * G::WS];            // 16-bit pixels (4 channels), 13.4 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbands = a.batch * G::NBANDS;
 
@@ -147,8 +256,8 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
         uint32_t o[8];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          o[2 * p] = u8_bf16(px[p] & 255u) | (u8_bf16((px[p] >> 8) & 255u) << 16);
-          o[2 * p + 1] = u8_bf16((px[p] >> 16) & 255u) | (u8_bf16(px[p] >> 24) << 16);
+          o[2 * p] = u8pair<NS>(px[p] & 255u, (px[p] >> 8) & 255u);
+          o[2 * p + 1] = u8pair<NS>((px[p] >> 16) & 255u, px[p] >> 24);
         }
         reinterpret_cast<uint4*>(xs)[2 * f] = make_uint4(o[0], o[1], o[2], o[3]);
         reinterpret_cast<uint4*>(xs)[2 * f + 1] = make_uint4(o[4], o[5], o[6], o[7]);
@@ -160,15 +269,15 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
   if (band < nbands) load_band(band);
 
   const int li = lane & 15, lq = lane >> 4;
-  bf16x8 wf[G::NSPLIT][2][G::KSTEPS];
+  u32x4 wf[NS][2][G::KSTEPS];
 #pragma unroll
-  for (int sp = 0; sp < G::NSPLIT; ++sp)
+  for (int sp = 0; sp < NS; ++sp)
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
         const uint4 u = a.wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane];
-        wf[sp][nt][s] = as_bf16x8(make_uint2(u.x, u.y), make_uint2(u.z, u.w));
+        wf[sp][nt][s] = u32x4{u.x, u.y, u.z, u.w};
       }
   // this lane's row (window li>>2, sub li&3) of m-block 0 of the wave, per (kstep, tap half)
   const int wi = li >> 2, sub = li & 3;
@@ -183,13 +292,15 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
     }
 
   unsigned long long pos = 0;
-  const float inv255 = 1.0f / 255.0f;
+  // (sum_k u8 * w 2^kw) * (2^-kw / 255): scaling by a power of two commutes with the rounding
+  const float oscale = NS == 2 ? (1.0f / 255.0f) * exp2i(-a.wexp[0]) : 1.0f / 255.0f;
   for (; band < nbands; band += gridDim.x) {
     const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
     __syncthreads();                                 // previous band's LDS reads are done
     store_band();
     __syncthreads();
     if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
+    float bmax = 0.f;
 #pragma unroll
     for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
       f32x4 acc[G::MCH][2];
@@ -197,20 +308,21 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
       for (int j = 0; j < G::MCH; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
-        bf16x8 af[G::MCH];
+        u32x4 af[G::MCH];
 #pragma unroll
         for (int j = 0; j < G::MCH; ++j) {
           const int jj = ch * G::MCH + j;
           const int off = (jj / G::MBROW) * 2 * G::WS + (jj % G::MBROW) * 8;   // immediate
-          af[j] = as_bf16x8(xs[lb[s][0] + off], xs[lb[s][1] + off]);
+          const uint2 p0 = xs[lb[s][0] + off], p1 = xs[lb[s][1] + off];
+          af[j] = u32x4{p0.x, p0.y, p1.x, p1.y};
         }
 #pragma unroll
-        for (int sp = 0; sp < G::NSPLIT; ++sp)
+        for (int sp = 0; sp < NS; ++sp)
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
             for (int j = 0; j < G::MCH; ++j)
-              acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], wf[sp][nt][s], acc[j][nt], 0, 0, 0);
+              acc[j][nt] = SP::mfma(af[j], wf[sp][nt][s], acc[j][nt]);
       }
       // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nt*16 + li
 #pragma unroll
@@ -228,11 +340,14 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
           if (v2 > mx) { mx = v2; arg = 2; }
           if (v3 > mx) { mx = v3; arg = 3; }
           const size_t o = ((size_t)(img * (G::HO / 2) + ph) * (G::WO / 2) + pw) * G::COUT + nt * 16 + li;
-          a.out[o] = mx > 0.f ? mx * inv255 : 0.f;
+          const float out = mx > 0.f ? mx * oscale : 0.f;
+          bmax = fmaxf(bmax, out);
+          a.out[o] = out;
           if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
         }
       }
     }
+    amax_publish(a.amax_out, img, bmax, lane);
   }
   if (a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
@@ -241,25 +356,27 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
 // conv0 weight gradient (Conv2DBackpropFilter of conv0, train.py:177 under TF autodiff):
 //   dW[tap, c, o] = (1/255) * sum_{n, pixel p} u8[n, p + tap, c] * dY[n, p, o]
 // with dY the un-pooled output gradient (dP routed to each window's argmax, ReLU folded in).
-// M = (tap, c) = 100 rows (7 m-tiles), N = o (2 n-tiles), K = pixels; dY is split into three
-// bf16 planes (exact), the frames are exact in bf16, so 3 MFMAs per (m-tile, n-tile, 32 px).
+// M = (tap, c) = 100 rows (7 m-tiles), N = o (2 n-tiles), K = pixels; dY is split into NS
+// planes (NS = 3: bf16 hi/mid/lo; NS = 2: fp16 hi/lo of dY * 2^ky, ky from the dP0 tensor's
+// max), the frames are exact in either type, so NS MFMAs per (m-tile, n-tile, 32 px).
 //
 // Persistent workgroups walk bands of RB output rows.  LDS per band:
-//   X: two copies of the RB + 4 input rows, channel-planar bf16, copy h shifted left by h
+//   X: two copies of the RB + 4 input rows, channel-planar 16-bit, copy h shifted left by h
 //      pixels, so the 8 pixels a lane feeds for tap (kh, kw) start at an even column of copy
 //      kw & 1 (dword aligned);
-//   Y: the POOLED gradient dP of the band, split: [split][pooled row][o][pooled col] bf16,
+//   Y: the POOLED gradient dP of the band, split: [split][pooled row][o][pooled col] 16-bit,
 //      plus its argmax codes [pooled row][o][pooled col] u8 — a quarter of the un-pooled
-//      dY's bytes, so staging writes 4x less and three workgroups fit a CU.  The MFMA B
-//      fragment (8 un-pooled pixels = 4 windows x 2 sub-columns of one row) is un-pooled in
-//      registers: window j's dword is (v, v) & mask, mask = 0x0000FFFF / 0xFFFF0000 for the
-//      argmax sub-column, 0 when the argmax is in the other row or there is no gradient.
-//      o pitch 40 bf16 = 20 dwords: the 16 o of a lane group land on 16 distinct bank pairs.
+//      dY's bytes.  The MFMA B fragment (8 un-pooled pixels = 4 windows x 2 sub-columns of
+//      one row) is un-pooled in registers: window j's dword is (v, v) & mask, mask =
+//      0x0000FFFF / 0xFFFF0000 for the argmax sub-column, 0 when the argmax is in the other
+//      row or there is no gradient.  o pitch 40 = 20 dwords: the 16 o of a lane group land on
+//      16 distinct bank pairs.
 // K-step s of a band = pixels 32s .. 32s + 31 (row-major over the band), lane group q
 // supplies pixels 32s + 8q .. + 7 (one row, since 80 % 8 == 0); waves take K-steps
 // s = wave, wave + 4, ...  The next band's global loads are issued into registers before
 // the MFMA phase of the current one.  Each workgroup writes one partial slab (x 1/255).
 // ---------------------------------------------------------------------------------------
+template <int NS>
 struct Conv0W {
   static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
   static constexpr int HO = 80, WO = 80, PH = 40, PW = 40;
@@ -268,19 +385,21 @@ struct Conv0W {
   static constexpr int KPB = RB * WO;              // 640 pixels per band
   static constexpr int KSTEPS = KPB / 32;          // 20
   static constexpr int KSW = KSTEPS / 4;           // 5 per wave
-  static constexpr int Y_BF16 = 3 * PRB * COUT * PW;                  // 15360
+  static constexpr int Y_16 = NS * PRB * COUT * PW;                   // 16-bit words
   static constexpr int YC_BYTES = PRB * COUT * PW;                    // 5120
-  static constexpr int XP = 88;                    // row pitch (bf16)
+  static constexpr int XP = 88;                    // row pitch (16-bit)
   static constexpr int XPL = XROWS * XP;           // channel plane
   static constexpr int XCP = C * XPL;              // copy
-  static constexpr int X_BF16 = 2 * XCP;
-  static constexpr int LDS_U4 = ((Y_BF16 + X_BF16) * 2 + YC_BYTES) / 16;
+  static constexpr int X_16 = 2 * XCP;
+  static constexpr int LDS_U4 = ((Y_16 + X_16) * 2 + YC_BYTES) / 16;
   static constexpr int MT = 7, M = NTAP * C;
+  static constexpr int SLAB_U4 = 4 * M * COUT * 4 / 16;            // epilogue: 4 wave slabs
+  static constexpr int ALLOC_U4 = LDS_U4 > SLAB_U4 ? LDS_U4 : SLAB_U4;
   static constexpr int NITEM = COUT * PRB * (PW / 4) / 256;            // dP items per thread
   static constexpr int NXV = XROWS * WS * C / 16;                      // uint4 of frame rows
   static_assert(KSTEPS % 4 == 0 && COUT * PRB * (PW / 4) % 256 == 0 && NXV <= 256, "geom");
   static_assert(HO % RB == 0 && RB + KT - 1 + HO - RB <= HS, "band rows stay inside the frame");
-  static_assert(WO % 8 == 0 && ((Y_BF16 + X_BF16) * 2) % 16 == 0, "layout");
+  static_assert(WO % 8 == 0 && ((Y_16 + X_16) * 2) % 16 == 0, "layout");
 };
 
 struct Conv0WArgs {
@@ -289,17 +408,22 @@ struct Conv0WArgs {
   const uint8_t* code;     // argmax codes of dP0
   float* part;             // [gridDim.x][100][32] partial slabs
   int batch;
+  const uint32_t* amax_dp; // NS = 2: max |dP0| slots (global at [0])
 };
 
+template <int NS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv0s_wgrad_kernel(const Conv0WArgs a) {
-  using G = Conv0W;
-  __shared__ uint4 lds[G::LDS_U4];
+  using G = Conv0W<NS>;
+  using SP = SplitP<NS>;
+  __shared__ uint4 lds[G::ALLOC_U4];
   uint16_t* ys = reinterpret_cast<uint16_t*>(lds);
-  uint16_t* xs = ys + G::Y_BF16;
-  uint8_t* yc8 = reinterpret_cast<uint8_t*>(xs + G::X_BF16);
+  uint16_t* xs = ys + G::Y_16;
+  uint8_t* yc8 = reinterpret_cast<uint8_t*>(xs + G::X_16);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int nbands = a.batch * G::NBANDS;
+  const int ky = NS == 2 ? amax_exp(a.amax_dp[0]) : 0;
+  const float ysc = exp2i(ky);
 
   // ---- per-thread prefetch registers for one band ----
   float yv[G::NITEM][4];
@@ -328,14 +452,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
     for (int i = 0; i < G::NITEM; ++i) {
       const int f = tid + 256 * i, o = f & 31, rest = f >> 5;
       const int pr = rest / (G::PW / 4), q4 = rest - pr * (G::PW / 4);
-      uint32_t h0, m0, l0, h1, m1, l1;
-      split3x2(yv[i][0], yv[i][1], h0, m0, l0);
-      split3x2(yv[i][2], yv[i][3], h1, m1, l1);
+      uint32_t s0[NS], s1[NS];
+      SP::split(yv[i][0], yv[i][1], ysc, s0);
+      SP::split(yv[i][2], yv[i][3], ysc, s1);
       const int e = (pr * G::COUT + o) * G::PW + 4 * q4;
-      constexpr int SP = G::PRB * G::COUT * G::PW;
-      *reinterpret_cast<uint2*>(ys + e) = make_uint2(h0, h1);
-      *reinterpret_cast<uint2*>(ys + SP + e) = make_uint2(m0, m1);
-      *reinterpret_cast<uint2*>(ys + 2 * SP + e) = make_uint2(l0, l1);
+      constexpr int SPL = G::PRB * G::COUT * G::PW;
+#pragma unroll
+      for (int sp = 0; sp < NS; ++sp)
+        *reinterpret_cast<uint2*>(ys + sp * SPL + e) = make_uint2(s0[sp], s1[sp]);
       *reinterpret_cast<uint32_t*>(yc8 + e) = yc[i];
     }
     if (tid < G::NXV) {
@@ -345,7 +469,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
       for (int c = 0; c < 4; ++c) {
         uint32_t b[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = u8_bf16((px[j] >> (8 * c)) & 255u);
+        for (int j = 0; j < 4; ++j) b[j] = u8pair<NS>((px[j] >> (8 * c)) & 255u, 0u) & 0xFFFFu;
         uint16_t* p0 = xs + c * G::XPL + r * G::XP + x;              // copy 0
         *reinterpret_cast<uint2*>(p0) = make_uint2(b[0] | (b[1] << 16), b[2] | (b[3] << 16));
         uint16_t* p1 = xs + G::XCP + c * G::XPL + r * G::XP + x;     // copy 1: column x - 1
@@ -356,7 +480,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
     }
   };
 
-  // per-lane A offsets (bf16 units) for m-tile mt: row m = 16 mt + li = (tap, c)
+  // per-lane A offsets (16-bit units) for m-tile mt: row m = 16 mt + li = (tap, c)
   int aoff[G::MT];
 #pragma unroll
   for (int mt = 0; mt < G::MT; ++mt) {
@@ -382,17 +506,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
       const int s = wave + 4 * i;
       const int pb = 32 * s + 8 * lq, r = pb / G::WO, x0 = pb - r * G::WO;
       const int xo = r * G::XP + x0;
-      bf16x8 av[G::MT];
+      u32x4 av[G::MT];
 #pragma unroll
       for (int mt = 0; mt < G::MT; ++mt) {
         const uint32_t* p = reinterpret_cast<const uint32_t*>(xs + aoff[mt] + xo);
-        const u32x4 u = {p[0], p[1], p[2], p[3]};
-        av[mt] = __builtin_bit_cast(bf16x8, u);
+        av[mt] = u32x4{p[0], p[1], p[2], p[3]};
       }
       // B: un-pool 4 windows (pooled cols x0/2 .. +3 of pooled row r/2) for channel o
       const uint32_t sy = (uint32_t)(r & 1);
       const int e0 = ((r >> 1) * G::COUT + li) * G::PW + (x0 >> 1);
-      bf16x8 bv[3][2];
+      u32x4 bv[NS][2];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int e = e0 + 16 * nt * G::PW;
@@ -404,29 +527,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
           mk[j] = (k >> 1) == sy ? ((k & 1u) ? 0xFFFF0000u : 0x0000FFFFu) : 0u;
         }
 #pragma unroll
-        for (int sp = 0; sp < 3; ++sp) {
+        for (int sp = 0; sp < NS; ++sp) {
           const uint2 u = *reinterpret_cast<const uint2*>(ys + sp * (G::PRB * G::COUT * G::PW) + e);
           // (lo, lo) and (hi, hi) half-word pairs of each dword
-          const u32x4 w = {__builtin_amdgcn_perm(u.x, u.x, 0x01000100u) & mk[0],
-                           __builtin_amdgcn_perm(u.x, u.x, 0x03020302u) & mk[1],
-                           __builtin_amdgcn_perm(u.y, u.y, 0x01000100u) & mk[2],
-                           __builtin_amdgcn_perm(u.y, u.y, 0x03020302u) & mk[3]};
-          bv[sp][nt] = __builtin_bit_cast(bf16x8, w);
+          bv[sp][nt] = u32x4{__builtin_amdgcn_perm(u.x, u.x, 0x01000100u) & mk[0],
+                             __builtin_amdgcn_perm(u.x, u.x, 0x03020302u) & mk[1],
+                             __builtin_amdgcn_perm(u.y, u.y, 0x01000100u) & mk[2],
+                             __builtin_amdgcn_perm(u.y, u.y, 0x03020302u) & mk[3]};
         }
       }
 #pragma unroll
-      for (int sp = 0; sp < 3; ++sp)
+      for (int sp = 0; sp < NS; ++sp)
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt)
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt], bv[sp][nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = SP::mfma(av[mt], bv[sp][nt], acc[mt][nt]);
     }
   }
 
   // ---- epilogue: the four waves' accumulators go through LDS and are summed in wave order
   // into ONE slab per workgroup (lane holds rows 16 mt + 4 lq + r, column 16 nt + li) ----
-  static_assert(4 * G::M * G::COUT * 4 <= G::LDS_U4 * 16, "slab staging fits the band LDS");
+  static_assert(4 * G::M * G::COUT * 4 <= G::ALLOC_U4 * 16, "slab staging fits the band LDS");
   float* red = reinterpret_cast<float*>(lds);
   __syncthreads();                                     // last band's LDS reads are done
 #pragma unroll
@@ -440,10 +562,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
       }
   __syncthreads();
   float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
-  const float inv255 = 1.0f / 255.0f;
+  const float oscale = (1.0f / 255.0f) * exp2i(-ky);
   for (int e = tid; e < G::M * G::COUT; e += 256) {
     constexpr int W = G::M * G::COUT;
-    pz[e] = (((red[e] + red[W + e]) + red[2 * W + e]) + red[3 * W + e]) * inv255;
+    pz[e] = (((red[e] + red[W + e]) + red[2 * W + e]) + red[3 * W + e]) * oscale;
   }
 }
 

@@ -34,8 +34,9 @@ __device__ __forceinline__ uint2 lds_tr16(const char* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
-template <int HS_, int WS_, int CIN_, int COUT_, int RB_, int CW_, int OW_, int PX_, int PY_>
+template <int HS_, int WS_, int CIN_, int COUT_, int RB_, int CW_, int OW_, int PX_, int PY_, int NS_ = 3>
 struct Wg6Geom {
+  static constexpr int NS = NS_;                          // split planes (3 bf16 / 2 fp16)
   static constexpr int HS = HS_, WS = WS_, CIN = CIN_, COUT = COUT_, RB = RB_, CW = CW_, OW = OW_;
   static constexpr int KH = 5, KW = 5, NTAP = 25;
   static constexpr int HO = HS - KH + 1, WO = WS - KW + 1, PH = HO / 2, PW = WO / 2;
@@ -51,7 +52,7 @@ struct Wg6Geom {
   static constexpr int TW = TBASE + (TREM > 0);
   static constexpr int M = NTAP * CIN;
   static_assert(CW == 16 && OW == 32, "16 input x 32 output channels per workgroup");
-  static_assert(PX >= 3 * XSB && PY >= 3 * YSB && PX % 8 == 0 && PY % 8 == 0, "pitches");
+  static_assert(PX >= NS * XSB && PY >= NS * YSB && PX % 8 == 0 && PY % 8 == 0, "pitches");
   static_assert(X_BYTES % 16 == 0 && RB % 2 == 0, "wgrad6 geometry");
 };
 
@@ -61,12 +62,18 @@ struct Wg6Args {
   const uint8_t* code;     // argmax codes of dP (255 = no gradient)
   float* part;             // [gridDim.x][M][COUT] partial slabs
   int batch;
+  const uint32_t* amax_x;  // NS = 2: max |X| slots (global at [0])
+  const uint32_t* amax_dp; // NS = 2: max |dP| slots (global at [0])
 };
 
 template <class G>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wgrad6_kernel(const Wg6Args a) {
+  using SP = SplitP<G::NS>;
   __shared__ uint4 lds4[(G::X_BYTES + G::Y_BYTES) / 16];
   char* xs = reinterpret_cast<char*>(lds4);
+  // NS = 2: both operands scaled by their whole tensor's max (the sum runs over images)
+  const int kx = G::NS == 2 ? amax_exp(a.amax_x[0]) : 0, ky = G::NS == 2 ? amax_exp(a.amax_dp[0]) : 0;
+  const float xsc = exp2i(kx), ysc = exp2i(ky);
   char* ys = xs + G::X_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cg = blockIdx.y / G::NOG, og = blockIdx.y - cg * G::NOG;
@@ -131,13 +138,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
       const int f = tid + 256 * i;
       if (f < XN) {
         const int pix = f / XQ, cq = f - pix * XQ;
-        uint32_t h0, m0, l0, h1, m1, l1;
-        split3x2(xv[i].x, xv[i].y, h0, m0, l0);
-        split3x2(xv[i].z, xv[i].w, h1, m1, l1);
+        uint32_t s0[G::NS], s1[G::NS];
+        SP::split(xv[i].x, xv[i].y, xsc, s0);
+        SP::split(xv[i].z, xv[i].w, xsc, s1);
         char* p = xs + pix * G::PX + cq * 8;
-        *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2*>(p + G::XSB) = make_uint2(m0, m1);
-        *reinterpret_cast<uint2*>(p + 2 * G::XSB) = make_uint2(l0, l1);
+#pragma unroll
+        for (int sp = 0; sp < G::NS; ++sp)
+          *reinterpret_cast<uint2*>(p + sp * G::XSB) = make_uint2(s0[sp], s1[sp]);
       }
     }
 #pragma unroll
@@ -150,13 +157,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
         float e[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == s ? e[k] : 0.f;
-        uint32_t h0, m0, l0, h1, m1, l1;
-        split3x2(e[0], e[1], h0, m0, l0);
-        split3x2(e[2], e[3], h1, m1, l1);
+        uint32_t s0[G::NS], s1[G::NS];
+        SP::split(e[0], e[1], ysc, s0);
+        SP::split(e[2], e[3], ysc, s1);
         char* d = ys + p * G::PY + oq * 8;
-        *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2*>(d + G::YSB) = make_uint2(m0, m1);
-        *reinterpret_cast<uint2*>(d + 2 * G::YSB) = make_uint2(l0, l1);
+#pragma unroll
+        for (int sp = 0; sp < G::NS; ++sp)
+          *reinterpret_cast<uint2*>(d + sp * G::YSB) = make_uint2(s0[sp], s1[sp]);
       }
     }
   };
@@ -184,14 +191,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
         const int y = p / G::WO, x = p - y * G::WO;
         xb[r] = (y * G::WS + x) * G::PX + 8 * pq;
       }
-      bf16x8 b[2][3];
+      u32x4 b[2][G::NS];
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-        for (int sp = 0; sp < 3; ++sp) {
+        for (int sp = 0; sp < G::NS; ++sp) {
           const uint2 u0 = lds_tr16(ys + yb[0] + nb * 32 + sp * G::YSB);
           const uint2 u1 = lds_tr16(ys + yb[1] + nb * 32 + sp * G::YSB);
-          b[nb][sp] = as_bf16x8(u0, u1);
+          b[nb][sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
         }
 #pragma unroll
       for (int t = 0; t < G::TW; ++t) {
@@ -199,32 +206,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
         const int tap = tap0 + t;
         const int kh = tap / G::KW, kw = tap - kh * G::KW;
         const int toff = (kh * G::WS + kw) * G::PX;
-        bf16x8 av[3];
+        u32x4 av[G::NS];
 #pragma unroll
-        for (int sp = 0; sp < 3; ++sp) {
+        for (int sp = 0; sp < G::NS; ++sp) {
           const uint2 u0 = lds_tr16(xs + xb[0] + toff + sp * G::XSB);
           const uint2 u1 = lds_tr16(xs + xb[1] + toff + sp * G::XSB);
-          av[sp] = as_bf16x8(u0, u1);
+          av[sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
         }
-        // a1b1, a1b2, a2b1, a1b3, a2b2, a3b1 — interleaved over the two n-blocks
+        // the family's cross products, interleaved over the two n-blocks
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[nb][0], acc[t][nb], 0, 0, 0);
+        for (int pr = 0; pr < SP::NPROD; ++pr)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[nb][1], acc[t][nb], 0, 0, 0);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[nb][0], acc[t][nb], 0, 0, 0);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], b[nb][2], acc[t][nb], 0, 0, 0);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], b[nb][1], acc[t][nb], 0, 0, 0);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], b[nb][0], acc[t][nb], 0, 0, 0);
+          for (int nb = 0; nb < 2; ++nb)
+            acc[t][nb] = SP::mfma(av[SP::pa(pr)], b[nb][SP::pb(pr)], acc[t][nb]);
       }
     }
   }
 
   // ---- epilogue: C layout 16x16: lane holds column (lane & 15) = o, rows 4*(lane>>4)+r = c ----
   float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
+  const float us1 = exp2i(-kx), us2 = exp2i(-ky);
 #pragma unroll
   for (int t = 0; t < G::TW; ++t) {
     if (t >= ntap) break;
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = c0 + 4 * (lane >> 4) + r;
-        pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[t][nb][r];
+        pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[t][nb][r] * us1 * us2;
       }
     }
   }
