@@ -462,7 +462,7 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3 = prm + h->tensors[h->idx_conv[3]].offset;
   unsigned long long* rc = train ? w.relu : nullptr;
-  uint32_t* am_p0 = w.am(AM_P0, h);
+  uint32_t* am_p0 = NS == 2 ? w.am(AM_P0, h) : nullptr;
   const SplitIO io1{AM_P0, 0, AM_P1}, io2{AM_P1, 1, -1};
   if (h->band) CHECK(launch_wprep<NS>(h, s, prm, w, train));
   if (train) {
@@ -622,7 +622,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
     CHECK(conv_reduce(pl, 3, 64, 64));
-    ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0, w.am(AM_DP2, h)};
+    ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0,
+                                           NS == 2 ? w.am(AM_DP2, h) : nullptr};
     CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
     CHECK(fork());
   }

@@ -43,17 +43,29 @@ __device__ __forceinline__ void relu_count_add_uniform(unsigned long long* slots
 }
 
 // Max |x| of a tensor, published for the scaled-fp16 split kernels that consume it
-// (ba3c_split.h): lane 0 of a wave adds the wave's max of image img to slot [1 + img] and to
-// the global slot [0] (atomicMax on the bits of a non-negative float orders like the float).
+// (ba3c_split.h): lane 0 of a wave adds the wave's max of image img to slot [1 + img]
+// (atomicMax on the bits of a non-negative float orders like the float; a few tens of waves
+// per image, so the adds do not contend — one chip-wide slot measured +0.2 ms per producer).
 // Every lane of the wave must call it (wave-wide reduction).
 __device__ __forceinline__ void amax_publish(uint32_t* slots, int img, float m, int lane) {
   if (!slots) return;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if (lane == 0 && m > 0.f) {
-    atomicMax(slots + 1 + img, __float_as_uint(m));
-    atomicMax(slots, __float_as_uint(m));
-  }
+  if (lane == 0 && m > 0.f) atomicMax(slots + 1 + img, __float_as_uint(m));
+}
+
+// The whole tensor's max (bits) from its per-image slots [1, 1 + B), for every thread of a
+// 256-thread workgroup (red4: 4 words of LDS).
+__device__ __forceinline__ uint32_t amax_all(const uint32_t* slots, int B, uint32_t* red4) {
+  uint32_t m = 0;
+  for (int i = threadIdx.x; i < B; i += 256) m = max(m, slots[1 + i]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+  __syncthreads();
+  const uint32_t r = max(max(red4[0], red4[1]), max(red4[2], red4[3]));
+  __syncthreads();
+  return r;
 }
 
 // dY at conv-output position (y, x) from pooled grad dP and argmax codes.

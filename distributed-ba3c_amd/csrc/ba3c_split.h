@@ -76,7 +76,7 @@ __device__ __forceinline__ void split3x2(float a, float b, uint32_t& hi, uint32_
 // multiplied by 2^-(ka + kb) in the epilogue.  The activation / gradient maps are scaled PER
 // IMAGE (the results of an image do not depend on the batch it runs in), weights per tensor,
 // and the weight-gradient kernels use the whole tensor's max.  Producers publish the maxima
-// (amax_publish) into per-image slots [1 + img] and a global slot [0].
+// (amax_publish) into per-image slots [1 + img]; the weight-gradient kernels reduce them.
 // ---------------------------------------------------------------------------------------
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
         }
       }
     }
-    amax_publish(a.amax_out, img, bmax, lane);
+    if constexpr (NS == 2) amax_publish(a.amax_out, img, bmax, lane);
   }
   if (a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
@@ -408,7 +408,7 @@ struct Conv0WArgs {
   const uint8_t* code;     // argmax codes of dP0
   float* part;             // [gridDim.x][100][32] partial slabs
   int batch;
-  const uint32_t* amax_dp; // NS = 2: max |dP0| slots (global at [0])
+  const uint32_t* amax_dp; // NS = 2: per-image max |dP0| slots
 };
 
 template <int NS>
@@ -422,7 +422,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int nbands = a.batch * G::NBANDS;
-  const int ky = NS == 2 ? amax_exp(a.amax_dp[0]) : 0;
+  __shared__ uint32_t red4[4];
+  const int ky = NS == 2 ? amax_exp(amax_all(a.amax_dp, a.batch, red4)) : 0;
   const float ysc = exp2i(ky);
 
   // ---- per-thread prefetch registers for one band ----

@@ -62,8 +62,8 @@ struct Wg6Args {
   const uint8_t* code;     // argmax codes of dP (255 = no gradient)
   float* part;             // [gridDim.x][M][COUT] partial slabs
   int batch;
-  const uint32_t* amax_x;  // NS = 2: max |X| slots (global at [0])
-  const uint32_t* amax_dp; // NS = 2: max |dP| slots (global at [0])
+  const uint32_t* amax_x;  // NS = 2: per-image max |X| slots
+  const uint32_t* amax_dp; // NS = 2: per-image max |dP| slots
 };
 
 template <class G>
@@ -72,7 +72,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
   __shared__ uint4 lds4[(G::X_BYTES + G::Y_BYTES) / 16];
   char* xs = reinterpret_cast<char*>(lds4);
   // NS = 2: both operands scaled by their whole tensor's max (the sum runs over images)
-  const int kx = G::NS == 2 ? amax_exp(a.amax_x[0]) : 0, ky = G::NS == 2 ? amax_exp(a.amax_dp[0]) : 0;
+  __shared__ uint32_t red4[4];
+  const int kx = G::NS == 2 ? amax_exp(amax_all(a.amax_x, a.batch, red4)) : 0;
+  const int ky = G::NS == 2 ? amax_exp(amax_all(a.amax_dp, a.batch, red4)) : 0;
   const float xsc = exp2i(kx), ysc = exp2i(ky);
   char* ys = xs + G::X_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
