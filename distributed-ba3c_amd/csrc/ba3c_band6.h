@@ -29,8 +29,11 @@ namespace ba3c {
 // With KPH < CIN the band is staged in CIN/KPH channel phases through the same LDS (smaller
 // footprint => more workgroups per CU to hide the staging); accumulators persist across
 // phases, so a phased layout needs all of a wave's m-blocks in one chunk.
-template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0, int NS_ = 3>
+template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0, int NS_ = 3, bool DBUF_ = false>
 struct Band6 {
+  // DBUF: A fragments of k-step t + 1 read into a second register set before k-step t's
+  // MFMAs (only where the registers allow it without spilling)
+  static constexpr bool DBUF = DBUF_;
   using G = G_;
   static constexpr int NS = NS_;                         // split planes (3 bf16 / 2 fp16)
   static constexpr int KPH = KPH_ ? KPH_ : G_::CIN;
@@ -62,87 +65,82 @@ struct Band6Args {
   uint32_t* amax_out;
 };
 
+// One workgroup = one band (image x RB output rows); two workgroups per CU overlap one's
+// staging with the other's MFMAs.  (A persistent variant with the next band prefetched into
+// registers spilled at these register budgets and measured slower: r02f)
 template <class L>
-__global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6_kernel(const Band6Args a) {
   using G = typename L::G;
+  using SP = SplitP<L::NS>;
   __shared__ uint4 lds4[L::LDS_BYTES / 16];
   char* lds = reinterpret_cast<char*>(lds4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int bid = blockIdx.x;
-  const int img = bid / G::NBANDS;
-  const int bnd = bid - img * G::NBANDS;
-  const int y0 = bnd * G::RB;
-  const int rows_out = min(G::RB, G::HO - y0);
+  const int band = blockIdx.x;
 
-  // ---- stage input rows [y0, y0 + rows_out + KH - 1), channels of phase ph, split into
-  // three bf16 planes ----
-  // Index math is 32-bit from per-workgroup base pointers (the band of an SRC 0 map is one
-  // contiguous run of rows); unsigned division by the compile-time Q / WS is a mul-hi.
-  using SP = SplitP<L::NS>;
-  const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
-  const float asc = exp2i(ka);
-  auto stage = [&](int ph) {
-    constexpr unsigned Q = L::KPH / 4;                   // float4 per pixel and phase
-    const int cb = ph * L::KPH;
-    constexpr int NTOT = (G::SROWS * G::WS * Q + 255) / 256;
-    constexpr int NPT = NTOT < 8 ? NTOT : 8;
+  // ---- staging of input rows [y0, y0 + rows_out + KH - 1) (channels of phase ph), split
+  // into NS planes.  Index math is 32-bit from per-band base pointers (the band of an SRC 0
+  // map is one contiguous run of rows); unsigned division by the compile-time Q / WS is a
+  // mul-hi.  SRC 1 un-pools (dP, code) on the fly (sub = position in the 2x2 window).
+  constexpr unsigned Q = L::KPH / 4;                     // float4 per pixel and phase
+  constexpr int NTOT = (G::SROWS * G::WS * Q + 255) / 256;
+  auto band_geom = [](int b, int& img, int& y0, int& rows_out) {
+    img = b / G::NBANDS;
+    y0 = (b - img * G::NBANDS) * G::RB;
+    rows_out = min(G::RB, G::HO - y0);
+  };
+  auto load1 = [&](int img, int y0, int rows_out, int cb, unsigned f, float4& v, uint32_t& cd) {
     const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * Q;
-    const float* srcb = G::SRC == 0 ? a.src + ((size_t)(img * G::HS + y0) * G::WS) * G::CIN + cb
-                                    : a.src + (size_t)img * (G::UPH * G::UPW) * G::CIN + cb;
-    const uint8_t* codeb = G::SRC == 1 ? a.code + (size_t)img * (G::UPH * G::UPW) * G::CIN + cb : nullptr;
-    for (int base = 0; base < NTOT; base += NPT) {
-      float4 v[NPT];
-      uint32_t cd[G::SRC == 1 ? NPT : 1];
-      uint32_t sub[G::SRC == 1 ? NPT : 1];
-#pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const unsigned f = tid + 256u * (base + i);
-        const unsigned pix = f / Q, cq = f - pix * Q;
-        v[i] = f4zero();
-        if constexpr (G::SRC == 0) {
-          if (f < nvec) v[i] = *reinterpret_cast<const float4*>(srcb + pix * G::CIN + cq * 4);
-        } else {
-          const unsigned ry = pix / G::WS, x = pix - ry * G::WS;
-          const int uy = (int)(y0 + ry) - G::PADY, ux = (int)x - G::PADX;
-          sub[i] = 4u;                                     // matches no code
-          cd[i] = 0;
-          if (f < nvec && (unsigned)uy < (unsigned)G::UHO && (unsigned)ux < (unsigned)G::UWO) {
-            const unsigned off = ((uy >> 1) * G::UPW + (ux >> 1)) * G::CIN + cq * 4;
-            v[i] = *reinterpret_cast<const float4*>(srcb + off);
-            cd[i] = *reinterpret_cast<const uint32_t*>(codeb + off);
-            sub[i] = ((uy & 1) << 1) | (ux & 1);
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const unsigned f = tid + 256u * (base + i);
-        if (f < nvec) {
-          const unsigned pix = f / Q, cq = f - pix * Q;
-          const unsigned ry = pix / G::WS;
-          float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-          if constexpr (G::SRC == 1) {
-            const uint32_t sb = sub[i], c = cd[i];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == sb ? e[k] : 0.f;
-          }
-          uint32_t s0[L::NS], s1[L::NS];
-          SP::split(e[0], e[1], asc, s0);
-          SP::split(e[2], e[3], asc, s1);
-          // ry * RP + x * PP == pix * PP + ry * (RP - WS * PP)
-          char* p = lds + pix * L::PP + ry * (L::RP - G::WS * L::PP) + cq * 8;
-#pragma unroll
-          for (int sp = 0; sp < L::NS; ++sp)
-            *reinterpret_cast<uint2*>(p + sp * L::SPB) = make_uint2(s0[sp], s1[sp]);
-        }
+    const unsigned pix = f / Q, cq = f - pix * Q;
+    v = f4zero();
+    cd = 0;
+    if constexpr (G::SRC == 0) {
+      const float* srcb = a.src + ((size_t)(img * G::HS + y0) * G::WS) * G::CIN + cb;
+      if (f < nvec) v = *reinterpret_cast<const float4*>(srcb + pix * G::CIN + cq * 4);
+    } else {
+      const unsigned ry = pix / G::WS, x = pix - ry * G::WS;
+      const int uy = (int)(y0 + ry) - G::PADY, ux = (int)x - G::PADX;
+      if (f < nvec && (unsigned)uy < (unsigned)G::UHO && (unsigned)ux < (unsigned)G::UWO) {
+        const size_t ib = (size_t)img * (G::UPH * G::UPW) * G::CIN + cb;
+        const unsigned off = ((uy >> 1) * G::UPW + (ux >> 1)) * G::CIN + cq * 4;
+        v = *reinterpret_cast<const float4*>(a.src + ib + off);
+        cd = *reinterpret_cast<const uint32_t*>(a.code + ib + off);
       }
     }
   };
-  if constexpr (L::NPH == 1) {
-    stage(0);
-    __syncthreads();
-  }
-
+  auto store1 = [&](int y0, int rows_out, unsigned f, const float4& v, uint32_t cd, float asc) {
+    const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * Q;
+    if (f >= nvec) return;
+    const unsigned pix = f / Q, cq = f - pix * Q;
+    const unsigned ry = pix / G::WS;
+    float e[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (G::SRC == 1) {
+      const unsigned x = pix - ry * G::WS;
+      const int uy = (int)(y0 + ry) - G::PADY, ux = (int)x - G::PADX;
+      const uint32_t sb = ((uy & 1) << 1) | (ux & 1);      // cd == 0 outside: no code matches
+      const bool in = (unsigned)uy < (unsigned)G::UHO && (unsigned)ux < (unsigned)G::UWO;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) e[k] = (in && ((cd >> (8 * k)) & 255u) == sb) ? e[k] : 0.f;
+    }
+    uint32_t s0[L::NS], s1[L::NS];
+    SP::split(e[0], e[1], asc, s0);
+    SP::split(e[2], e[3], asc, s1);
+    // ry * RP + x * PP == pix * PP + ry * (RP - WS * PP)
+    char* p = lds + pix * L::PP + ry * (L::RP - G::WS * L::PP) + cq * 8;
+#pragma unroll
+    for (int sp = 0; sp < L::NS; ++sp) *reinterpret_cast<uint2*>(p + sp * L::SPB) = make_uint2(s0[sp], s1[sp]);
+  };
+  // staging: loads in chunks of NPT, then their stores
+  auto stage = [&](int img, int y0, int rows_out, int ph, float asc) {
+    constexpr int NPT = NTOT < 8 ? NTOT : 8;
+    for (int base = 0; base < NTOT; base += NPT) {
+      float4 v[NPT];
+      uint32_t cd[NPT];
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) load1(img, y0, rows_out, ph * L::KPH, tid + 256u * (base + i), v[i], cd[i]);
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) store1(y0, rows_out, tid + 256u * (base + i), v[i], cd[i], asc);
+    }
+  };
   const int nb = wave % G::NB;
   const int mb0 = wave / G::NB;
   const int li = lane & 15, lq = lane >> 4;
@@ -153,8 +151,17 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
   // K index (tap, channel) of k-step t of a phase, relative to the phase's first channel
   auto koff = [](int t) { return (t / L::K32) * G::CIN + (t % L::K32) * 32; };
   unsigned long long pos = 0;
-  const float us1 = exp2i(-ka), us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
+  const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
+
+  int img, y0, rows_out;
+  band_geom(band, img, y0, rows_out);
+  const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
+  const float asc = exp2i(ka), us1 = exp2i(-ka);
   float omax = 0.f;
+  if constexpr (L::NPH == 1) {
+    stage(img, y0, rows_out, 0, asc);
+    __syncthreads();
+  }
 
 #pragma unroll
   for (int chn = 0; chn < L::NCH; ++chn) {
@@ -187,33 +194,22 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
     for (int ph = 0; ph < L::NPH; ++ph) {
     if constexpr (L::NPH > 1) {
       if (ph) __syncthreads();                            // previous phase's reads are done
-      stage(ph);
+      stage(img, y0, rows_out, ph, asc);
       __syncthreads();
     }
     const uint16_t* wph = wrow + ph * L::KPH;
-    constexpr int LA = 2;
+    constexpr int LA = 3;
     uint4 bring[LA + 1][L::NS];
 #pragma unroll
     for (int t = 0; t < LA && t < L::NT; ++t)
 #pragma unroll
       for (int s = 0; s < L::NS; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
-#pragma unroll
-    for (int t = 0; t < L::NT; ++t) {
-      if (t + LA < L::NT) {
-#pragma unroll
-        for (int s = 0; s < L::NS; ++s)
-          bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t + LA));
-      }
-      u32x4 b[L::NS];
-#pragma unroll
-      for (int s = 0; s < L::NS; ++s) {
-        const uint4 u = bring[t % (LA + 1)][s];
-        b[s] = u32x4{u.x, u.y, u.z, u.w};
-      }
+    // A fragments double-buffered in registers: k-step t + 1's LDS reads are issued before
+    // k-step t's MFMAs, so their latency hides behind the MFMA chain
+    auto read_a = [&](int t, u32x4 (&av)[L::NS][MCH]) {
       const int tap = t / L::K32, ch = t - tap * L::K32;
       const int kh = tap / G::KW, kw = tap - kh * G::KW;
       const int toff = kh * L::RP + kw * L::PP + ch * 64;
-      u32x4 av[L::NS][MCH];
 #pragma unroll
       for (int j = 0; j < MCH; ++j)
 #pragma unroll
@@ -221,12 +217,35 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
           const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * L::SPB);
           av[s][j] = u32x4{u.x, u.y, u.z, u.w};
         }
+    };
+    constexpr int NB2 = L::DBUF ? 2 : 1;
+    u32x4 avb[NB2][L::NS][MCH];
+    if constexpr (L::DBUF) read_a(0, avb[0]);
+#pragma unroll
+    for (int t = 0; t < L::NT; ++t) {
+      if (t + LA < L::NT) {
+#pragma unroll
+        for (int s = 0; s < L::NS; ++s)
+          bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t + LA));
+      }
+      if constexpr (L::DBUF) {
+        if (t + 1 < L::NT) read_a(t + 1, avb[(t + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);                // keep those reads ahead of the MFMAs
+      } else {
+        read_a(t, avb[0]);
+      }
+      u32x4 b[L::NS];
+#pragma unroll
+      for (int s = 0; s < L::NS; ++s) {
+        const uint4 u = bring[t % (LA + 1)][s];
+        b[s] = u32x4{u.x, u.y, u.z, u.w};
+      }
       // NS = 3: a1b1, a1b2, a2b1, a1b3, a2b2, a3b1;  NS = 2: a1b1, a1b2, a2b1 —
       // interleaved over m-blocks
 #pragma unroll
       for (int pr = 0; pr < SP::NPROD; ++pr)
 #pragma unroll
-        for (int j = 0; j < MCH; ++j) acc[j] = SP::mfma(av[SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
+        for (int j = 0; j < MCH; ++j) acc[j] = SP::mfma(avb[L::DBUF ? (t & 1) : 0][SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
     }
     }
 
@@ -241,7 +260,7 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
         const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
         const float v0 = acc[j][0], v1 = acc[j][1], v2 = acc[j][2], v3 = acc[j][3];
         if (w * 4 < G::MROWS && 2 * ph < rows_out) {
-          pos += count_pos4(v0, v1, v2, v3);   // wave-uniform
+          pos += count_pos4(v0, v1, v2, v3);   // uniform over the active lanes (lane 0 among them)
           float mx = v0;
           uint32_t arg = 0;
           if (v1 > mx) { mx = v1; arg = 1; }
@@ -267,8 +286,8 @@ __global__ void __launch_bounds__(256) conv_band6_kernel(const Band6Args a) {
       }
     }
   }
-  if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
   if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
+  if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
 
 // One launch per step for all weight preparation on the split path: job y < njobs writes the

@@ -130,12 +130,12 @@ struct Lay<3> {
 };
 template <>
 struct Lay<2> {
-  using C1F = Band6<GConv1F, 160, 128, 7, 0, 2>;
+  using C1F = Band6<GConv1F, 160, 128, 7, 0, 2, true>;
   using C2F = Band6<GConv2F, 160, 64, 7, 0, 2>;
-  using C1D = Band6<GConv1D, 160, 128, 5, 0, 2>;
+  using C1D = Band6<GConv1D, 160, 128, 5, 0, 2, true>;
   using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2>;
-  using C2FS = Band6<GConv2FS, 160, 64, 2, 0, 2>;
-  using C2DS = Band6<GConv2DS, 160, 128, 2, 32, 2>;
+  using C2FS = Band6<GConv2FS, 160, 64, 2, 0, 2, true>;
+  using C2DS = Band6<GConv2DS, 160, 128, 2, 32, 2, true>;
   using W1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 160, 2>;
   using W2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 160, 2>;
 };
@@ -782,6 +782,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = (e[0] == '1');
   if (const char* e = getenv("BA3C_SPLIT")) h->ns = (std::strcmp(e, "bf16") == 0) ? 3 : 2;
+
   if (!(h->band && h->b6 && h->w6 && h->split)) h->ns = 3;
 
   const int F = c.fc_neurons, per = F / splits;
