@@ -13,3 +13,4 @@ $S 500 gpurun_out/$T/bench.log python bench.py && \
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && \
 $S 300 gpurun_out/$T/rocprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/stats -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-b32 --no-overlap
 tail -3 gpurun_out/$T/pytest_gpu.log; tail -1 gpurun_out/$T/smoke.log; grep '^{' gpurun_out/$T/bench.log | cut -c1-1500
+cd $GRAFT_REPO_ROOT && $S 300 gpurun_out/$T/rocprof32.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/stats32 -o run -- python bench.py --batch 32 --fc_neurons 128 --fc_splits 4 --steps 50 --warmup 5 --no-cpu-baseline --no-b32 --no-overlap
