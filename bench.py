@@ -305,17 +305,22 @@ def main():
     roof = None
     if dom_flops:
         split = tr.engine.kernel_split(dom)
+        fam = tr.engine.kernel_family(dom)
         peak = kernel_peak(split)
         ach = dom_flops / (avg_ms / 1000.0) / 1e12
+        if split <= 1:
+            path = "fp32 MFMA"
+        elif fam == 2:
+            path = "fp16 MFMA, %d products per fp32 product (power-of-two scaled hi/lo split)" % split
+        else:
+            path = "bf16 MFMA, %d products per fp32 product (exact hi/mid/lo split)" % split
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
                 "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "traffic": pmc_traffic(dom), "avg_launch_ms": round(avg_ms, 4),
-                "launches": launches,
-                "path": "fp32 MFMA" if split <= 1 else
-                        "bf16 MFMA, %d products per fp32 product (exact split)" % split,
+                "launches": launches, "path": path,
                 "peak_basis": "algorithmic fp32 FLOP/s: %s" % (
                     "fp32 MFMA 157.3 TF" if split <= 1 else
-                    "2516.6 TF dense bf16 / %d split products" % split)}
+                    "2516.6 TF dense 16-bit MFMA / %d split products" % split)}
     step_tflops = train_step_flops(B, C, F, A) / (ms_step / 1000.0) / 1e12
 
     out = {"metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,

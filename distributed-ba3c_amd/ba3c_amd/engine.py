@@ -214,9 +214,14 @@ class Ba3cEngine(object):
         _lib.check(self.lib.ba3c_probe_enable(self.h, kid))
 
     def kernel_split(self, kernel):
-        """bf16 MFMA products per fp32 product of `kernel` on this handle (6: bf16x6 split,
-        3: conv0's u8 x bf16x3 split, 1: fp32 MFMA, 0: no matrix work)."""
+        """16-bit MFMA products per fp32 product of `kernel` on this handle (6: bf16 hi/mid/lo,
+        3: scaled fp16 hi/lo or conv0's u8 x bf16x3, 2: conv0's u8 x fp16 hi/lo, 1: fp32 MFMA,
+        0: no matrix work)."""
         return int(self.lib.ba3c_kernel_split(self.h, _lib.KERNEL_IDS[kernel]))
+
+    def kernel_family(self, kernel):
+        """3: bf16 split planes, 2: scaled fp16 split planes, else kernel_split's value."""
+        return int(self.lib.ba3c_kernel_family(self.h, _lib.KERNEL_IDS[kernel]))
 
     def probe_read(self):
         ms, n = ctypes.c_double(), ctypes.c_int32()

@@ -17,6 +17,7 @@
 #include "../../include/ba3c.h"
 #include "ba3c_band6.h"
 #include "ba3c_conv.h"
+#include "ba3c_gemm6.h"
 #include "ba3c_problems.h"
 #include "ba3c_rollout.h"
 #include "ba3c_small.h"
@@ -71,6 +72,8 @@ struct ba3c_handle {
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  bool g6 = true;     // implicit-GEMM launches (conv3, fc1, heads; C=12 conv0) on bf16x6 split
+                      // MFMA (ba3c_gemm6.h; BA3C_GEMM6=0 or BA3C_GENERIC=1: fp32 MFMA)
   // split family of the split kernels: 2 = scaled fp16 hi/lo, 3 MFMAs per fp32 product
   // (default); 3 = bf16 hi/mid/lo, 6 MFMAs (BA3C_SPLIT=bf16).  The fp16 family needs every
   // producer of a split operand to publish its max, so it is used only when all split
@@ -286,7 +289,10 @@ int launch_gemm(ba3c_handle* h, hipStream_t s, int kid, const P& p, int splits) 
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
   {
     ProbeScope ps(h, s, kid);
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, P>), grid, dim3(GEMM_THREADS), 0, s, p);
+    if (h->g6)
+      hipLaunchKernelGGL((gemm6_kernel<BM, BN, WGM, WGN, P>), grid, dim3(GEMM_THREADS), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, P>), grid, dim3(GEMM_THREADS), 0, s, p);
   }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
@@ -523,8 +529,11 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
            h->cfg.replace_with_conv ? 0 : 1, B, F, 1600, FC_KCHUNK, w.fcpart};
   {
     ProbeScope ps(h, s, BA3C_K_FC1_FWD);
-    hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, FcFwd>), dim3((B + 127) / 128, (F + 63) / 64, FC_SPLIT),
-                       dim3(GEMM_THREADS), 0, s, fc);
+    const dim3 grid((B + 127) / 128, (F + 63) / 64, FC_SPLIT);
+    if (h->g6)
+      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);
+    else
+      hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);
     const int nblk = (int)std::min<size_t>(((size_t)B * F + 255) / 256, 2048);
     hipLaunchKernelGGL(fc_finish_kernel, dim3(nblk), dim3(256), 0, s, fc, FC_SPLIT);
   }
@@ -781,6 +790,8 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = (e[0] == '1');
+  if (const char* e = getenv("BA3C_GEMM6")) h->g6 = !(e[0] == '0');
+  if (!h->band) h->g6 = false;
   if (const char* e = getenv("BA3C_SPLIT")) h->ns = (std::strcmp(e, "bf16") == 0) ? 3 : 2;
 
   if (!(h->band && h->b6 && h->w6 && h->split)) h->ns = 3;
@@ -1136,19 +1147,38 @@ int ba3c_kernel_split(const ba3c_handle* h, int32_t kid) {
   const bool c4 = h->cfg.channels == 4;
   switch (kid) {
     case BA3C_K_CONV0_FWD:
-    case BA3C_K_CONV0_WGRAD: return (h->band && c4 && h->split) ? h->ns : 1;
+    case BA3C_K_CONV0_WGRAD: return (h->band && c4 && h->split) ? h->ns : (h->g6 ? 6 : 1);
     case BA3C_K_CONV1_FWD:
     case BA3C_K_CONV2_FWD:
     case BA3C_K_CONV1_DGRAD:
     case BA3C_K_CONV2_DGRAD: return (h->band && h->b6) ? (h->ns == 2 ? 3 : 6) : 1;
     case BA3C_K_CONV1_WGRAD:
     case BA3C_K_CONV2_WGRAD: return (h->band && h->w6) ? (h->ns == 2 ? 3 : 6) : 1;
+    case BA3C_K_CONV3_FWD:
+    case BA3C_K_CONV3_DGRAD:
+    case BA3C_K_CONV3_WGRAD:
+    case BA3C_K_FC1_FWD:
+    case BA3C_K_FC1_DGRAD:
+    case BA3C_K_FC1_WGRAD:
+    case BA3C_K_HEAD_WGRAD: return h->g6 ? 6 : 1;
     case BA3C_K_HEADS:
     case BA3C_K_WGRAD_REDUCE:
     case BA3C_K_CLIP:
     case BA3C_K_UPDATE: return 0;
     default: return 1;
   }
+}
+
+int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {
+  if (!h || kid < 0 || kid >= BA3C_NUM_KERNELS) return -1;
+  const int sp = ba3c_kernel_split(h, kid);
+  if (sp <= 1) return sp;
+  const bool band_split = kid == BA3C_K_CONV0_FWD || kid == BA3C_K_CONV0_WGRAD || kid == BA3C_K_CONV1_FWD ||
+                          kid == BA3C_K_CONV2_FWD || kid == BA3C_K_CONV1_DGRAD || kid == BA3C_K_CONV2_DGRAD ||
+                          kid == BA3C_K_CONV1_WGRAD || kid == BA3C_K_CONV2_WGRAD;
+  if (kid == BA3C_K_CONV0_FWD || kid == BA3C_K_CONV0_WGRAD)
+    if (!(h->band && h->cfg.channels == 4 && h->split)) return 3;
+  return band_split && h->ns == 2 ? 2 : 3;
 }
 
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches) {

@@ -179,10 +179,15 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
 
 /* Arithmetic path of kernel `kernel_id` on this handle (for roofline accounting; no
- * reference counterpart): the number of bf16 MFMA products it issues per fp32 product —
- * 6 for the bf16x6 split (fp32-accurate), 3 for conv0's exact u8 x bf16x3 split — or 1 for
- * fp32 MFMA (v_mfma_f32_*_f32), 0 for a kernel with no matrix work; -1 on a bad id. */
+ * reference counterpart): the number of 16-bit MFMA products it issues per fp32 product —
+ * 6 for the bf16 hi/mid/lo split, 3 for the scaled fp16 hi/lo split (or conv0's u8 x bf16x3),
+ * 2 for conv0's u8 x scaled-fp16 hi/lo — or 1 for fp32 MFMA (v_mfma_f32_*_f32), 0 for a
+ * kernel with no matrix work; -1 on a bad id. */
 int ba3c_kernel_split(const ba3c_handle* h, int32_t kernel_id);
+
+/* Operand family of a split kernel: 3 = bf16 planes (v_mfma_*_bf16), 2 = power-of-two
+ * scaled fp16 planes (v_mfma_*_f16); otherwise the value of ba3c_kernel_split (1, 0, -1). */
+int ba3c_kernel_family(const ba3c_handle* h, int32_t kernel_id);
 
 /* ---- data formats either side of the path ---------------- */
 
