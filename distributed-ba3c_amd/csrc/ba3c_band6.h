@@ -65,30 +65,28 @@ struct Band6Args {
   uint32_t* amax_out;
 };
 
-// One workgroup = one band (image x RB output rows); two workgroups per CU overlap one's
-// staging with the other's MFMAs.  (A persistent variant with the next band prefetched into
-// registers spilled at these register budgets and measured slower: r02f)
+// Staging and compute of one band, shared by the one-band-per-workgroup kernel and the
+// pipelined persistent kernel below.
 template <class L>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6_kernel(const Band6Args a) {
+struct Band6Ops {
   using G = typename L::G;
   using SP = SplitP<L::NS>;
-  __shared__ uint4 lds4[L::LDS_BYTES / 16];
-  char* lds = reinterpret_cast<char*>(lds4);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int band = blockIdx.x;
+  static constexpr unsigned Q = L::KPH / 4;                 // float4 per pixel and phase
+  static constexpr int NTOT = (G::SROWS * G::WS * Q + 255) / 256;
 
-  // ---- staging of input rows [y0, y0 + rows_out + KH - 1) (channels of phase ph), split
-  // into NS planes.  Index math is 32-bit from per-band base pointers (the band of an SRC 0
-  // map is one contiguous run of rows); unsigned division by the compile-time Q / WS is a
-  // mul-hi.  SRC 1 un-pools (dP, code) on the fly (sub = position in the 2x2 window).
-  constexpr unsigned Q = L::KPH / 4;                     // float4 per pixel and phase
-  constexpr int NTOT = (G::SROWS * G::WS * Q + 255) / 256;
-  auto band_geom = [](int b, int& img, int& y0, int& rows_out) {
+  __device__ static void band_geom(int b, int& img, int& y0, int& rows_out) {
     img = b / G::NBANDS;
     y0 = (b - img * G::NBANDS) * G::RB;
     rows_out = min(G::RB, G::HO - y0);
-  };
-  auto load1 = [&](int img, int y0, int rows_out, int cb, unsigned f, float4& v, uint32_t& cd) {
+  }
+
+  // ---- staging of input rows [y0, y0 + rows_out + KH - 1) (channels of phase ph), split
+  // into NS planes, by 256 threads (t = 0..255).  Index math is 32-bit from per-band base
+  // pointers (the band of an SRC 0 map is one contiguous run of rows); unsigned division by
+  // the compile-time Q / WS is a mul-hi.  SRC 1 un-pools (dP, code) on the fly (sub =
+  // position in the 2x2 window).
+  __device__ static void load1(const Band6Args& a, int img, int y0, int rows_out, int cb, unsigned f,
+                               float4& v, uint32_t& cd) {
     const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * Q;
     const unsigned pix = f / Q, cq = f - pix * Q;
     v = f4zero();
@@ -106,8 +104,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
         cd = *reinterpret_cast<const uint32_t*>(a.code + ib + off);
       }
     }
-  };
-  auto store1 = [&](int y0, int rows_out, unsigned f, const float4& v, uint32_t cd, float asc) {
+  }
+  __device__ static void store1(char* lds, int y0, int rows_out, unsigned f, const float4& v, uint32_t cd,
+                                float asc) {
     const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * Q;
     if (f >= nvec) return;
     const unsigned pix = f / Q, cq = f - pix * Q;
@@ -128,166 +127,244 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
     char* p = lds + pix * L::PP + ry * (L::RP - G::WS * L::PP) + cq * 8;
 #pragma unroll
     for (int sp = 0; sp < L::NS; ++sp) *reinterpret_cast<uint2*>(p + sp * L::SPB) = make_uint2(s0[sp], s1[sp]);
-  };
-  // staging: loads in chunks of NPT, then their stores
-  auto stage = [&](int img, int y0, int rows_out, int ph, float asc) {
-    constexpr int NPT = NTOT < 8 ? NTOT : 8;
+  }
+  // loads in chunks of NPT (<= NPTMAX), then their stores
+  template <int NPTMAX = 8>
+  __device__ static void stage(const Band6Args& a, char* lds, int t, int img, int y0, int rows_out, int ph,
+                               float asc) {
+    constexpr int NPT = NTOT < NPTMAX ? NTOT : NPTMAX;
     for (int base = 0; base < NTOT; base += NPT) {
       float4 v[NPT];
       uint32_t cd[NPT];
 #pragma unroll
-      for (int i = 0; i < NPT; ++i) load1(img, y0, rows_out, ph * L::KPH, tid + 256u * (base + i), v[i], cd[i]);
+      for (int i = 0; i < NPT; ++i) load1(a, img, y0, rows_out, ph * L::KPH, t + 256u * (base + i), v[i], cd[i]);
 #pragma unroll
-      for (int i = 0; i < NPT; ++i) store1(y0, rows_out, tid + 256u * (base + i), v[i], cd[i], asc);
+      for (int i = 0; i < NPT; ++i) store1(lds, y0, rows_out, t + 256u * (base + i), v[i], cd[i], asc);
     }
-  };
-  const int nb = wave % G::NB;
-  const int mb0 = wave / G::NB;
-  const int li = lane & 15, lq = lane >> 4;
-  const int col = nb * 16 + li;
-  // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] 16-bit
-  const uint16_t* wrow = a.wt6 + (size_t)col * G::KDIM + 8 * lq;
-  constexpr size_t WSPLIT = (size_t)G::COUT * G::KDIM;
-  // K index (tap, channel) of k-step t of a phase, relative to the phase's first channel
-  auto koff = [](int t) { return (t / L::K32) * G::CIN + (t % L::K32) * 32; };
-  unsigned long long pos = 0;
-  const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
-
-  int img, y0, rows_out;
-  band_geom(band, img, y0, rows_out);
-  const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
-  const float asc = exp2i(ka), us1 = exp2i(-ka);
-  float omax = 0.f;
-  if constexpr (L::NPH == 1) {
-    stage(img, y0, rows_out, 0, asc);
-    __syncthreads();
   }
 
+  // ---- MFMA main loop + epilogue of one band by the 4 compute waves (wave = 0..3).  For a
+  // phased layout (NPH > 1) `stage_phase(ph)` stages phase ph between the barriers; with
+  // NPH == 1 the band must already be in LDS.  ReLU positives add to `pos`, the band's max
+  // |out| to `omax`.
+  template <class StageFn>
+  __device__ static void compute(const Band6Args& a, const char* lds, int wave, int lane, int img, int y0,
+                                 int rows_out, float us1, float us2, unsigned long long& pos, float& omax,
+                                 StageFn&& stage_phase) {
+    // lane-derived addressing goes through an empty asm: recomputed per band (a few VALU)
+    // instead of being hoisted out of a persistent caller's band loop into live registers
+    asm volatile("" : "+v"(lane));
+    const int nb = wave % G::NB;
+    const int mb0 = wave / G::NB;
+    const int li = lane & 15, lq = lane >> 4;
+    const int col = nb * 16 + li;
+    // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] 16-bit.  The
+    // offset goes through an empty asm so a persistent caller's band loop cannot hoist the
+    // (band-invariant) weight loads of all k-steps out of the loop into registers.
+    int woff = col * G::KDIM + 8 * lq;
+    asm volatile("" : "+v"(woff));
+    const uint16_t* wrow = a.wt6 + woff;
+    constexpr size_t WSPLIT = (size_t)G::COUT * G::KDIM;
+    // K index (tap, channel) of k-step t of a phase, relative to the phase's first channel
+    auto koff = [](int t) { return (t / L::K32) * G::CIN + (t % L::K32) * 32; };
+
 #pragma unroll
-  for (int chn = 0; chn < L::NCH; ++chn) {
-    constexpr int MCH = L::MCH;
-    int abase[MCH];                                       // bytes
-    bool live[MCH];
+    for (int chn = 0; chn < L::NCH; ++chn) {
+      constexpr int MCH = L::MCH;
+      int abase[MCH];                                       // bytes
+      bool live[MCH];
 #pragma unroll
-    for (int j = 0; j < MCH; ++j) {
-      const int mb = mb0 + (chn * MCH + j) * G::WPN;
-      const int row = mb * 16 + li;
-      int oy, ox;
-      if constexpr (G::POOL) {
-        const int w = row >> 2, sb = row & 3;
-        const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
-        oy = 2 * ph + (sb >> 1);
-        ox = 2 * pw + (sb & 1);
-      } else {
-        oy = row / G::WO;
-        ox = row - oy * G::WO;
+      for (int j = 0; j < MCH; ++j) {
+        const int mb = mb0 + (chn * MCH + j) * G::WPN;
+        const int row = mb * 16 + li;
+        int oy, ox;
+        if constexpr (G::POOL) {
+          const int w = row >> 2, sb = row & 3;
+          const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
+          oy = 2 * ph + (sb >> 1);
+          ox = 2 * pw + (sb & 1);
+        } else {
+          oy = row / G::WO;
+          ox = row - oy * G::WO;
+        }
+        live[j] = chn * MCH + j < G::MBW && mb < G::MB;
+        const bool ok = live[j] && row < G::MROWS && oy < rows_out;
+        abase[j] = (ok ? oy * L::RP + ox * L::PP : 0) + 16 * lq;
       }
-      live[j] = chn * MCH + j < G::MBW && mb < G::MB;
-      const bool ok = live[j] && row < G::MROWS && oy < rows_out;
-      abase[j] = (ok ? oy * L::RP + ox * L::PP : 0) + 16 * lq;
-    }
-    f32x4 acc[MCH];
+      f32x4 acc[MCH];
 #pragma unroll
-    for (int j = 0; j < MCH; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < MCH; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
-    for (int ph = 0; ph < L::NPH; ++ph) {
-    if constexpr (L::NPH > 1) {
-      if (ph) __syncthreads();                            // previous phase's reads are done
-      stage(img, y0, rows_out, ph, asc);
-      __syncthreads();
-    }
-    const uint16_t* wph = wrow + ph * L::KPH;
-    constexpr int LA = 3;
-    uint4 bring[LA + 1][L::NS];
+      for (int ph = 0; ph < L::NPH; ++ph) {
+        if constexpr (L::NPH > 1) stage_phase(ph);
+        const uint16_t* wph = wrow + ph * L::KPH;
+        constexpr int LA = 3;
+        uint4 bring[LA + 1][L::NS];
 #pragma unroll
-    for (int t = 0; t < LA && t < L::NT; ++t)
+        for (int t = 0; t < LA && t < L::NT; ++t)
 #pragma unroll
-      for (int s = 0; s < L::NS; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
-    // A fragments double-buffered in registers: k-step t + 1's LDS reads are issued before
-    // k-step t's MFMAs, so their latency hides behind the MFMA chain
-    auto read_a = [&](int t, u32x4 (&av)[L::NS][MCH]) {
-      const int tap = t / L::K32, ch = t - tap * L::K32;
-      const int kh = tap / G::KW, kw = tap - kh * G::KW;
-      const int toff = kh * L::RP + kw * L::PP + ch * 64;
+          for (int s = 0; s < L::NS; ++s) bring[t][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t));
+        // A fragments double-buffered in registers: k-step t + 1's LDS reads are issued before
+        // k-step t's MFMAs, so their latency hides behind the MFMA chain
+        auto read_a = [&](int t, u32x4 (&av)[L::NS][MCH]) {
+          const int tap = t / L::K32, ch = t - tap * L::K32;
+          const int kh = tap / G::KW, kw = tap - kh * G::KW;
+          const int toff = kh * L::RP + kw * L::PP + ch * 64;
 #pragma unroll
-      for (int j = 0; j < MCH; ++j)
+          for (int j = 0; j < MCH; ++j)
 #pragma unroll
-        for (int s = 0; s < L::NS; ++s) {
-          const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * L::SPB);
-          av[s][j] = u32x4{u.x, u.y, u.z, u.w};
+            for (int s = 0; s < L::NS; ++s) {
+              const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * L::SPB);
+              av[s][j] = u32x4{u.x, u.y, u.z, u.w};
+            }
+        };
+        constexpr int NB2 = L::DBUF ? 2 : 1;
+        u32x4 avb[NB2][L::NS][MCH];
+        if constexpr (L::DBUF) read_a(0, avb[0]);
+#pragma unroll
+        for (int t = 0; t < L::NT; ++t) {
+          if (t + LA < L::NT) {
+#pragma unroll
+            for (int s = 0; s < L::NS; ++s)
+              bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t + LA));
+          }
+          if constexpr (L::DBUF) {
+            if (t + 1 < L::NT) read_a(t + 1, avb[(t + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);                // keep those reads ahead of the MFMAs
+          } else {
+            read_a(t, avb[0]);
+          }
+          u32x4 b[L::NS];
+#pragma unroll
+          for (int s = 0; s < L::NS; ++s) {
+            const uint4 u = bring[t % (LA + 1)][s];
+            b[s] = u32x4{u.x, u.y, u.z, u.w};
+          }
+          // NS = 3: a1b1, a1b2, a2b1, a1b3, a2b2, a3b1;  NS = 2: a1b1, a1b2, a2b1 —
+          // interleaved over m-blocks
+#pragma unroll
+          for (int pr = 0; pr < SP::NPROD; ++pr)
+#pragma unroll
+            for (int j = 0; j < MCH; ++j) acc[j] = SP::mfma(avb[L::DBUF ? (t & 1) : 0][SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
         }
-    };
-    constexpr int NB2 = L::DBUF ? 2 : 1;
-    u32x4 avb[NB2][L::NS][MCH];
-    if constexpr (L::DBUF) read_a(0, avb[0]);
-#pragma unroll
-    for (int t = 0; t < L::NT; ++t) {
-      if (t + LA < L::NT) {
-#pragma unroll
-        for (int s = 0; s < L::NS; ++s)
-          bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t + LA));
       }
-      if constexpr (L::DBUF) {
-        if (t + 1 < L::NT) read_a(t + 1, avb[(t + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);                // keep those reads ahead of the MFMAs
-      } else {
-        read_a(t, avb[0]);
-      }
-      u32x4 b[L::NS];
-#pragma unroll
-      for (int s = 0; s < L::NS; ++s) {
-        const uint4 u = bring[t % (LA + 1)][s];
-        b[s] = u32x4{u.x, u.y, u.z, u.w};
-      }
-      // NS = 3: a1b1, a1b2, a2b1, a1b3, a2b2, a3b1;  NS = 2: a1b1, a1b2, a2b1 —
-      // interleaved over m-blocks
-#pragma unroll
-      for (int pr = 0; pr < SP::NPROD; ++pr)
-#pragma unroll
-        for (int j = 0; j < MCH; ++j) acc[j] = SP::mfma(avb[L::DBUF ? (t & 1) : 0][SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
-    }
-    }
 
-    // ---- epilogue (16x16 C layout: lane holds column li, rows 4 lq + r) ----
-    // un-scale by 2^-(ka + kw) (two exact power-of-two products)
+      // ---- epilogue (16x16 C layout: lane holds column li, rows 4 lq + r) ----
+      // un-scale by 2^-(ka + kw) (two exact power-of-two products)
 #pragma unroll
-    for (int j = 0; j < MCH; ++j) {
-      const int mb = mb0 + (chn * MCH + j) * G::WPN;
-      if (!live[j]) continue;
-      if constexpr (G::POOL) {
-        const int w = mb * 4 + lq;
-        const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
-        const float v0 = acc[j][0], v1 = acc[j][1], v2 = acc[j][2], v3 = acc[j][3];
-        if (w * 4 < G::MROWS && 2 * ph < rows_out) {
-          pos += count_pos4(v0, v1, v2, v3);   // uniform over the active lanes (lane 0 among them)
-          float mx = v0;
-          uint32_t arg = 0;
-          if (v1 > mx) { mx = v1; arg = 1; }
-          if (v2 > mx) { mx = v2; arg = 2; }
-          if (v3 > mx) { mx = v3; arg = 3; }
-          const size_t o = ((size_t)(img * (G::HO / 2) + y0 / 2 + ph) * (G::WO / 2) + pw) * G::COUT + col;
-          const float out = fmaxf(mx, 0.f) * us1 * us2;
-          omax = fmaxf(omax, out);
-          a.out[o] = out;
-          if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
-        }
-      } else {
+      for (int j = 0; j < MCH; ++j) {
+        const int mb = mb0 + (chn * MCH + j) * G::WPN;
+        if (!live[j]) continue;
+        if constexpr (G::POOL) {
+          const int w = mb * 4 + lq;
+          const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
+          const float v0 = acc[j][0], v1 = acc[j][1], v2 = acc[j][2], v3 = acc[j][3];
+          if (w * 4 < G::MROWS && 2 * ph < rows_out) {
+            pos += count_pos4(v0, v1, v2, v3);   // uniform over the active lanes (lane 0 among them)
+            float mx = v0;
+            uint32_t arg = 0;
+            if (v1 > mx) { mx = v1; arg = 1; }
+            if (v2 > mx) { mx = v2; arg = 2; }
+            if (v3 > mx) { mx = v3; arg = 3; }
+            const size_t o = ((size_t)(img * (G::HO / 2) + y0 / 2 + ph) * (G::WO / 2) + pw) * G::COUT + col;
+            const float out = fmaxf(mx, 0.f) * us1 * us2;
+            omax = fmaxf(omax, out);
+            a.out[o] = out;
+            if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+          }
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mb * 16 + lq * 4 + r;
-          const int oy = row / G::WO, ox = row - oy * G::WO;
-          if (row < G::MROWS && oy < rows_out) {
-            const float out = acc[j][r] * us1 * us2;
-            omax = fmaxf(omax, fabsf(out));
-            a.out[((size_t)(img * G::HO + y0 + oy) * G::WO + ox) * G::COUT + col] = out;
+          for (int r = 0; r < 4; ++r) {
+            const int row = mb * 16 + lq * 4 + r;
+            const int oy = row / G::WO, ox = row - oy * G::WO;
+            if (row < G::MROWS && oy < rows_out) {
+              const float out = acc[j][r] * us1 * us2;
+              omax = fmaxf(omax, fabsf(out));
+              a.out[((size_t)(img * G::HO + y0 + oy) * G::WO + ox) * G::COUT + col] = out;
+            }
           }
         }
       }
     }
   }
+};
+
+// One workgroup = one band (image x RB output rows); two workgroups per CU overlap one's
+// staging with the other's MFMAs.
+template <class L>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6_kernel(const Band6Args a) {
+  using O = Band6Ops<L>;
+  __shared__ uint4 lds4[L::LDS_BYTES / 16];
+  char* lds = reinterpret_cast<char*>(lds4);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int img, y0, rows_out;
+  O::band_geom(blockIdx.x, img, y0, rows_out);
+  const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
+  const float asc = exp2i(ka), us1 = exp2i(-ka);
+  const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
+  unsigned long long pos = 0;
+  float omax = 0.f;
+  if constexpr (L::NPH == 1) {
+    O::stage(a, lds, tid, img, y0, rows_out, 0, asc);
+    __syncthreads();
+  }
+  O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [&](int ph) {
+    if (ph) __syncthreads();                                // previous phase's reads are done
+    O::stage(a, lds, tid, img, y0, rows_out, ph, asc);
+    __syncthreads();
+  });
   if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
-  if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
+  if (L::G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
+}
+
+// Pipelined persistent variant (NPH == 1 layouts): one 512-thread workgroup per CU walks
+// bands blockIdx.x, + gridDim.x, ...; waves 4..7 stage band i + 1 into one of two LDS
+// buffers while waves 0..3 run band i's MFMAs from the other, one barrier per band.  The
+// staging (global loads + split VALU + LDS stores) of the one-band kernel runs beside the
+// MFMA chain instead of before it.
+template <class L>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) conv_band6p_kernel(const Band6Args a) {
+  static_assert(L::NPH == 1, "pipelined band kernel: unphased layouts");
+  using O = Band6Ops<L>;
+  using G = typename L::G;
+  static_assert(2 * L::LDS_BYTES <= 160 * 1024, "two band buffers");
+  __shared__ uint4 lds4[2 * L::LDS_BYTES / 16];
+  char* buf0 = reinterpret_cast<char*>(lds4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform role branch
+  const bool loader = wave >= 4;
+  const int nbands = a.batch * G::NBANDS;
+  const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
+  auto scale_of = [&](int img) { return L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0; };
+  unsigned long long pos = 0;
+  int band = blockIdx.x;
+  if (loader && band < nbands) {
+    int img, y0, rows_out;
+    O::band_geom(band, img, y0, rows_out);
+    O::template stage<4>(a, buf0, tid - 256, img, y0, rows_out, 0, exp2i(scale_of(img)));
+  }
+  __syncthreads();
+  for (int i = 0; band < nbands; band += gridDim.x, ++i) {
+    char* cur = buf0 + (i & 1) * L::LDS_BYTES;
+    if (loader) {
+      const int nxt = band + gridDim.x;
+      if (nxt < nbands) {
+        int img, y0, rows_out;
+        O::band_geom(nxt, img, y0, rows_out);
+        O::template stage<4>(a, buf0 + ((i + 1) & 1) * L::LDS_BYTES, tid - 256, img, y0, rows_out, 0,
+                             exp2i(scale_of(img)));
+      }
+    } else {
+      int img, y0, rows_out;
+      O::band_geom(band, img, y0, rows_out);
+      float omax = 0.f;
+      O::compute(a, cur, wave, lane, img, y0, rows_out, exp2i(-scale_of(img)), us2, pos, omax, [](int) {});
+      if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
+    }
+    __syncthreads();
+  }
+  if (!loader && G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
 
 // One launch per step for all weight preparation on the split path: job y < njobs writes the
@@ -306,6 +383,7 @@ struct WPrep6Args {
   uint32_t* amax;          // max-|x| slots zeroed here (n_amax words; may be null)
   int n_amax;
   int* wexp;               // [5]: weight scale exponents of jobs 0..3 and conv0 (NS = 2)
+  int c0lay;               // conv0 forward LDS layout (its K order: conv0_wtap)
 };
 
 template <int NS>
@@ -324,7 +402,7 @@ __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
       k = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, red4)));
       if (blockIdx.x == 0 && threadIdx.x == 0) a.wexp[4] = k;
     }
-    conv0s_wprep_one<NS>(a.w0, a.wb0, blockIdx.x * 256 + threadIdx.x, k);
+    conv0s_wprep_one<NS>(a.w0, a.wb0, blockIdx.x * 256 + threadIdx.x, k, a.c0lay);
     return;
   }
   const WPrepJob& j = a.jobs.job[y];

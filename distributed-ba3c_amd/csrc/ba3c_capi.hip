@@ -72,6 +72,12 @@ struct ba3c_handle {
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  // conv1 fwd / dgrad on the pipelined persistent band kernel (BA3C_PIPE=1).  Off: r02e
+  // measured it slower (conv1 fwd 0.41 -> 0.51 ms, dgrad 0.43 -> 0.47 ms) — one compute wave
+  // per SIMD exposes the LDS-read latency that two co-resident one-band workgroups hide.
+  bool pipe = false;
+  int cus = 256;      // compute units of the device (persistent grids)
+  int c0lay = 2;      // conv0 forward LDS layout (ba3c_split.h; BA3C_C0LAY=0/1/2)
   bool g6 = true;     // implicit-GEMM launches (conv3, fc1, heads; C=12 conv0) on bf16x6 split
                       // MFMA (ba3c_gemm6.h; BA3C_GEMM6=0 or BA3C_GENERIC=1: fp32 MFMA)
   // split family of the split kernels: 2 = scaled fp16 hi/lo, 3 MFMAs per fp32 product
@@ -123,6 +129,7 @@ struct Lay;
 template <>
 struct Lay<3> {
   using C1F = Band6<GConv1F, 192, 32, 7, 0, 3>;
+  using C1FP = C1F;
   using C2F = Band6<GConv2F, 192, 32, 7, 0, 3>;
   using C1D = Band6<GConv1D, 224, 128, 5, 0, 3>;
   using C2D = Band6<GConv2DW, 224, 128, 11, 32, 3>;
@@ -134,6 +141,7 @@ struct Lay<3> {
 template <>
 struct Lay<2> {
   using C1F = Band6<GConv1F, 160, 128, 7, 0, 2, true>;
+  using C1FP = Band6<GConv1F, 160, 128, 7, 0, 2, false>;   // pipelined: no spill without DBUF
   using C2F = Band6<GConv2F, 160, 64, 7, 0, 2>;
   using C1D = Band6<GConv1D, 160, 128, 5, 0, 2, true>;
   using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2>;
@@ -331,25 +339,34 @@ struct SplitIO {
   int amax_in, wjob, amax_out;
 };
 
-template <class L>
+// LP: the layout of the pipelined persistent variant (conv_band6p_kernel), used when the
+// launch has >= 4 bands per CU
+template <class L, class LP = L>
 int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
-                 int wt_off, SplitIO io) {
+                 int wt_off, SplitIO io, bool pipelined = false) {
   const Band6Args b{a.src, a.code, w.wt6 + L::NS * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch,
                     w.am(io.amax_in, h), w.wexp + io.wjob, io.amax_out >= 0 ? w.am(io.amax_out, h) : nullptr};
-  dim3 grid(a.batch * L::G::NBANDS);
+  const int nbands = a.batch * L::G::NBANDS;
   {
     ProbeScope ps(h, s, kid);
-    hipLaunchKernelGGL(conv_band6_kernel<L>, grid, dim3(256), 0, s, b);
+    if constexpr (LP::NPH == 1 && 2 * LP::LDS_BYTES <= 160 * 1024) {
+      if (pipelined && h->pipe && nbands >= 4 * h->cus) {
+        hipLaunchKernelGGL(conv_band6p_kernel<LP>, dim3(std::min(nbands, h->cus)), dim3(512), 0, s, b);
+        HIP_TRY(hipGetLastError());
+        return BA3C_OK;
+      }
+    }
+    hipLaunchKernelGGL(conv_band6_kernel<L>, dim3(nbands), dim3(256), 0, s, b);
   }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
 
 // band conv: split MFMA when enabled, fp32 MFMA otherwise
-template <class L>
+template <class L, class LP = L>
 int launch_bandx(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
-                 int wt_off, SplitIO io) {
-  if (h->b6) return launch_band6<L>(h, s, kid, a, w, wt_off, io);
+                 int wt_off, SplitIO io, bool pipelined = false) {
+  if (h->b6) return launch_band6<L, LP>(h, s, kid, a, w, wt_off, io, pipelined);
   return launch_band<typename L::G>(h, s, kid, a);
 }
 
@@ -418,6 +435,7 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
     pa.amax = w.amax;
     pa.n_amax = AMAX_N * (1 + h->cfg.max_batch);
     pa.wexp = w.wexp;
+    pa.c0lay = h->c0lay;
     hipLaunchKernelGGL(wprep6_kernel<NS>, dim3(64, a.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
     HIP_TRY(hipGetLastError());
   } else {
@@ -428,7 +446,7 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
     if (!h->b6) {
       hipLaunchKernelGGL(conv0s_wprep_kernel, dim3((2 * Conv0S::KSTEPS * 64 + 255) / 256), dim3(256),
                          0, s, prm + h->tensors[h->idx_conv[0]].offset,
-                         reinterpret_cast<uint4*>(w.wt + WT_C0S));
+                         reinterpret_cast<uint4*>(w.wt + WT_C0S), h->c0lay);
       HIP_TRY(hipGetLastError());
     }
   } else if (h->cfg.channels == 4) {
@@ -446,8 +464,10 @@ int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a, const Wo
                         reinterpret_cast<const uint4*>(w.wt + WT_C0S), a.out, a.out_code,
                         a.relu_count, a.batch, w.wexp + 4, w.am(AM_P0, h)};
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-    hipLaunchKernelGGL(conv0s_fwd_kernel<NS>, dim3(std::min(FW_P0S, a.batch * Conv0S::NBANDS)), dim3(256), 0,
-                       s, sa);
+    const dim3 grid(std::min(FW_P0S, a.batch * Conv0S::NBANDS));
+    if (h->c0lay == 2) hipLaunchKernelGGL((conv0s_fwd_kernel<NS, 2>), grid, dim3(256), 0, s, sa);
+    else if (h->c0lay == 1) hipLaunchKernelGGL((conv0s_fwd_kernel<NS, 1>), grid, dim3(256), 0, s, sa);
+    else hipLaunchKernelGGL((conv0s_fwd_kernel<NS, 0>), grid, dim3(256), 0, s, sa);
   } else {
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
     hipLaunchKernelGGL(conv0_band_kernel, dim3(a.batch * Conv0Geom::NBANDS), dim3(256), 0, s, a);
@@ -481,9 +501,9 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
     }
     if (h->band) {
-      CHECK(launch_bandx<typename LY::C1F>(h, s, BA3C_K_CONV1_FWD,
+      CHECK((launch_bandx<typename LY::C1F, typename LY::C1FP>(h, s, BA3C_K_CONV1_FWD,
                                           BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}, w,
-                                          WT_C1F, io1));
+                                          WT_C1F, io1, true)));
       const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B};
       if (h->b6 && B <= SMALL_B)
         CHECK(launch_band6<typename LY::C2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
@@ -504,9 +524,9 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
                                                    B * 6400, 32, 25 * CH, 0, am_p0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
     }
-    CHECK(launch_bandx<typename LY::C1F>(h, s, BA3C_K_CONV1_FWD,
+    CHECK((launch_bandx<typename LY::C1F, typename LY::C1FP>(h, s, BA3C_K_CONV1_FWD,
                                         BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}, w,
-                                        WT_C1F, io1));
+                                        WT_C1F, io1, true)));
     const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B};
     if (h->b6 && B <= SMALL_B)
       CHECK(launch_band6<typename LY::C2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
@@ -681,7 +701,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
     if (h->band) {
       const BandArgs ba{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B};
-      CHECK(launch_bandx<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0}));
+      CHECK(launch_bandx<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0},
+                                          true));
     } else {
       ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
@@ -790,6 +811,14 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = (e[0] == '1');
+  if (const char* e = getenv("BA3C_PIPE")) h->pipe = (e[0] == '1');
+  {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      h->cus = n;
+  }
+  if (const char* e = getenv("BA3C_C0LAY")) h->c0lay = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("BA3C_GEMM6")) h->g6 = !(e[0] == '0');
   if (!h->band) h->g6 = false;
   if (const char* e = getenv("BA3C_SPLIT")) h->ns = (std::strcmp(e, "bf16") == 0) ? 3 : 2;

@@ -141,6 +141,9 @@ struct Conv0S {
   static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
   static constexpr int HO = 80, WO = 80, RB = 16, NBANDS = HO / RB, SROWS = RB + KT - 1;
   static constexpr int KSTEPS = 4;                 // 4 x 32 K = 32 tap slots (25 used)
+  // LDS row pitch (pixels) of layout LAY: 0 = dense 84 with taps in order (r01), 1 = 88 with
+  // taps in order, 2 = 88 with the paired tap order (conv0_atap); 704 B = 64 mod 256
+  __host__ __device__ static constexpr int xp(int lay) { return lay ? 88 : 84; }
   static constexpr int MAXSPLIT = 3;
   static constexpr int PROWS_W = RB / 2 / 4;       // pooled rows per wave (2)
   static constexpr int MBROW = (WO / 2) / 4;       // m-blocks per pooled row (10)
@@ -151,11 +154,33 @@ struct Conv0S {
   static_assert(RB % 8 == 0 && HO % RB == 0 && MBW % MCH == 0, "conv0 split geometry");
 };
 
+// K order of conv0's forward: slot (kstep s, lane group q, tap half h) -> tap.  Slot pair
+// p = 4s + 2(q >> 1) + h holds taps (p, p + 10) in lane groups q = 2(q >> 1) and + 1, i.e.
+// (kh, kw) and (kh + 2, kw): with the 88-pixel LDS row pitch (704 B = 64 mod 256) the four
+// 64-byte pixel runs a 32-lane half reads (2 rows x 2 lane groups) land in four distinct
+// bank windows, and a 16-lane group's two rows in two (ds_read_b64 / ds_read2_b64 both
+// conflict-free; r01 v7 measured 48 % conflict cycles on the 84-pixel, tap-order layout).
+// Pairs p = 10..14 carry only tap p + 10 (kh = 4): their even slot is padding (weight 0)
+// that reads tap p's address; pair 15 is padding in both slots (addresses of taps 0, 10).
+__host__ __device__ constexpr int conv0_pair(int s, int q, int h) { return 4 * s + 2 * (q >> 1) + h; }
+// the tap whose pixels slot (s, q, h) reads (always a real tap: in-bounds, finite values);
+// layouts 0 / 1 keep the plain order tap = 8s + 2q + h (padding slots read tap 0)
+__host__ __device__ constexpr int conv0_atap(int s, int q, int h, int lay = 2) {
+  return lay == 2 ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) : 0) + 10 * (q & 1)
+                  : (8 * s + 2 * q + h < 25 ? 8 * s + 2 * q + h : 0);
+}
+// the tap whose weight slot (s, q, h) carries, -1 for padding
+__host__ __device__ constexpr int conv0_wtap(int s, int q, int h, int lay = 2) {
+  return lay == 2 ? ((q & 1) ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) + 10 : -1)
+                             : (conv0_pair(s, q, h) < 10 ? conv0_pair(s, q, h) : -1))
+                  : (8 * s + 2 * q + h < 25 ? 8 * s + 2 * q + h : -1);
+}
+
 // real-channel weight of conv0/W [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99) at
-// K position (kstep s, lane group q, element e) = tap 8s + 2q + (e >> 2), channel e & 3
-__device__ __forceinline__ float conv0_w(const float* __restrict__ w, int s, int q, int e, int n) {
-  const int tap = 8 * s + 2 * q + (e >> 2), c = e & 3;
-  return tap < Conv0S::NTAP ? w[((size_t)tap * 16 + c) * 32 + n] : 0.f;
+// K position (kstep s, lane group q, element e) = tap conv0_wtap(s, q, e >> 2), channel e & 3
+__device__ __forceinline__ float conv0_w(const float* __restrict__ w, int s, int q, int e, int n, int lay) {
+  const int tap = conv0_wtap(s, q, e >> 2, lay), c = e & 3;
+  return tap >= 0 ? w[((size_t)tap * 16 + c) * 32 + n] : 0.f;
 }
 
 // max |w| over conv0's real-channel weights, reduced over the calling workgroup (256 threads)
@@ -176,7 +201,7 @@ __device__ __forceinline__ float conv0_wmax_block(const float* __restrict__ w, f
 // One thread per (nt, kstep, lane).
 template <int NS>
 __device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, uint4* __restrict__ wb, int t,
-                                                 int kexp) {
+                                                 int kexp, int lay = 2) {
   using G = Conv0S;
   if (t >= 2 * G::KSTEPS * 64) return;
   const int lane = t & 63, s = (t >> 6) % G::KSTEPS, nt = t / (64 * G::KSTEPS);
@@ -185,7 +210,7 @@ __device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, ui
   uint32_t part[NS][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const float v = conv0_w(w, s, q, e, n);
+    const float v = conv0_w(w, s, q, e, n, lay);
     if constexpr (NS == 3) split3(v, part[0][e], part[1][e], part[2][e]);
     else split2(v * sc, part[0][e], part[1][e]);
   }
@@ -197,8 +222,8 @@ __device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, ui
 }
 
 __global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restrict__ w,
-                                                           uint4* __restrict__ wb) {
-  conv0s_wprep_one<3>(w, wb, blockIdx.x * 256 + threadIdx.x, 0);
+                                                           uint4* __restrict__ wb, int lay) {
+  conv0s_wprep_one<3>(w, wb, blockIdx.x * 256 + threadIdx.x, 0, lay);
 }
 
 // Persistent workgroups walk bands (one image x RB output rows = RB/2 pooled rows); wave w
@@ -226,11 +251,12 @@ __device__ __forceinline__ uint32_t u8pair(uint32_t a, uint32_t b) {
   else return pack_f16x2((float)a, (float)b);
 }
 
-template <int NS>
+template <int NS, int LAY = 2>
 __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
   using G = Conv0S;
+  constexpr int XP = G::xp(LAY);
   using SP = SplitP<NS>;
-  __shared__ uint2 xs[G::SROWS * G::WS];            // 16-bit pixels (4 channels), 13.4 KB
+  __shared__ uint2 xs[G::SROWS * XP];               // 16-bit pixels (4 channels), 14 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbands = a.batch * G::NBANDS;
 
@@ -259,8 +285,9 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
           o[2 * p] = u8pair<NS>(px[p] & 255u, (px[p] >> 8) & 255u);
           o[2 * p + 1] = u8pair<NS>((px[p] >> 16) & 255u, px[p] >> 24);
         }
-        reinterpret_cast<uint4*>(xs)[2 * f] = make_uint4(o[0], o[1], o[2], o[3]);
-        reinterpret_cast<uint4*>(xs)[2 * f + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+        const int px0 = 4 * f, r = px0 / G::WS, lp = r * XP + (px0 - r * G::WS);   // 4 px of one row
+        reinterpret_cast<uint4*>(xs + lp)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        reinterpret_cast<uint4*>(xs + lp)[1] = make_uint4(o[4], o[5], o[6], o[7]);
       }
     }
   };
@@ -281,14 +308,14 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
       }
   // this lane's row (window li>>2, sub li&3) of m-block 0 of the wave, per (kstep, tap half)
   const int wi = li >> 2, sub = li & 3;
-  const int pix0 = (4 * wave + (sub >> 1)) * G::WS + 2 * wi + (sub & 1);
+  const int pix0 = (4 * wave + (sub >> 1)) * XP + 2 * wi + (sub & 1);
   int lb[G::KSTEPS][2];
 #pragma unroll
   for (int s = 0; s < G::KSTEPS; ++s)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int tap = 8 * s + 2 * lq + h;
-      lb[s][h] = pix0 + (tap < G::NTAP ? (tap / G::KT) * G::WS + tap % G::KT : 0);
+      const int tap = conv0_atap(s, lq, h, LAY);
+      lb[s][h] = pix0 + (tap / G::KT) * XP + tap % G::KT;
     }
 
   unsigned long long pos = 0;
@@ -312,7 +339,7 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
 #pragma unroll
         for (int j = 0; j < G::MCH; ++j) {
           const int jj = ch * G::MCH + j;
-          const int off = (jj / G::MBROW) * 2 * G::WS + (jj % G::MBROW) * 8;   // immediate
+          const int off = (jj / G::MBROW) * 2 * XP + (jj % G::MBROW) * 8;   // immediate
           const uint2 p0 = xs[lb[s][0] + off], p1 = xs[lb[s][1] + off];
           af[j] = u32x4{p0.x, p0.y, p1.x, p1.y};
         }
@@ -387,9 +414,12 @@ struct Conv0W {
   static constexpr int KSW = KSTEPS / 4;           // 5 per wave
   static constexpr int Y_16 = NS * PRB * COUT * PW;                   // 16-bit words
   static constexpr int YC_BYTES = PRB * COUT * PW;                    // 5120
-  static constexpr int XP = 88;                    // row pitch (16-bit)
-  static constexpr int XPL = XROWS * XP;           // channel plane
-  static constexpr int XCP = C * XPL;              // copy
+  // row / channel-plane / copy pitches (16-bit units) from a bank search over the A-fragment
+  // dword reads (2 x 32-lane groups, bank mod 32): 1.43 LDS cycles per read against 3.71 for
+  // the dense 88 / 1056 / 4224 layout (r01 v7: 65 % conflict cycles)
+  static constexpr int XP = 88;
+  static constexpr int XPL = 1072;                 // >= XROWS * XP = 1056
+  static constexpr int XCP = 4292;                 // >= C * XPL = 4288
   static constexpr int X_16 = 2 * XCP;
   static constexpr int LDS_U4 = ((Y_16 + X_16) * 2 + YC_BYTES) / 16;
   static constexpr int MT = 7, M = NTAP * C;

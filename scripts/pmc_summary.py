@@ -26,8 +26,8 @@ SHORT = [  # (regex on the kernel symbol, bench kernel id)
     (r"ConvDgrad<7, 7, 64", "conv3_dgrad"),
     (r"ConvWgrad<false, 7, 7, 64", "conv3_wgrad"),
     (r"FcFwd", "fc1_fwd"), (r"FcDgrad", "fc1_dgrad"),
-    (r"gemm_kernel<128, 64, 2, 2, ba3c::BatchWgrad", "fc1_wgrad"),
-    (r"gemm_kernel<128, 32, 4, 1, ba3c::BatchWgrad", "head_wgrad"),
+    (r"gemm6?_kernel<128, 64, 2, 2, ba3c::BatchWgrad", "fc1_wgrad"),
+    (r"gemm6?_kernel<128, 32, 4, 1, ba3c::BatchWgrad", "head_wgrad"),
     (r"heads_kernel", "heads"), (r"wgrad_reduce_kernel", "wgrad_reduce"),
     (r"update_kernel", "update"), (r"sumsq_kernel", "sumsq"),
 ]
