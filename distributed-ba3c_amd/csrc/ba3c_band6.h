@@ -408,12 +408,24 @@ __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
   const WPrepJob& j = a.jobs.job[y];
   float sc = 1.f;
   if constexpr (NS == 2) {
-    float m = 0.f;
+    // max |W| over the tensor (L2-resident): four independent float4 loads in flight per
+    // thread (a single dependent chain was ~15 us of the B=32 step)
     const float4* w4 = reinterpret_cast<const float4*>(j.w);
-    for (int i = threadIdx.x; i < j.n / 4; i += 256) {
-      const float4 v = w4[i];
-      m = fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+    auto amax4 = [](float m, const float4& v) {
+      return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+    };
+    const int n4 = j.n / 4;
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+    int i = threadIdx.x;
+    for (; i + 768 < n4; i += 1024) {
+      const float4 v0 = w4[i], v1 = w4[i + 256], v2 = w4[i + 512], v3 = w4[i + 768];
+      m0 = amax4(m0, v0);
+      m1 = amax4(m1, v1);
+      m2 = amax4(m2, v2);
+      m3 = amax4(m3, v3);
     }
+    for (; i < n4; i += 256) m0 = amax4(m0, w4[i]);
+    float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;

@@ -92,6 +92,9 @@ struct ba3c_handle {
   bool overlap = false;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
+  // weight-gradient reductions of the running backward pass, launched together at its end
+  bool defer_reduce = false;
+  ReduceJobs rjobs{};
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -164,7 +167,10 @@ constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64
               WT_TOTAL = WT_C0S + 4 * Conv0S::WB_U4;
 
 struct Workspace {
-  float *p0, *p1, *p2, *a3, *h, *fcpart, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part, *part0, *sumsq, *wt;
+  float *p0, *p1, *p2, *a3, *h, *fcpart, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part0, *sumsq, *wt;
+  // split-K / per-workgroup partial slabs of each weight gradient (reduced in one launch at the
+  // end of the backward pass, so each layer needs a region of its own)
+  float *part_h, *part_f, *part_3, *part_2, *part_1;
   uint16_t* wt6;   // [3][N][K] bf16 splits of the four band-conv weight copies
   uint8_t *c0, *c1, *c2;
   unsigned long long* relu;
@@ -212,20 +218,22 @@ size_t max_partials0(const ba3c_handle* h, int B) {
   return mx;
 }
 
-size_t max_partials(const ba3c_handle* h, int B) {
+// partial-slab floats of each layer's weight gradient (every kernel variant of that layer)
+struct PartialSizes {
+  size_t heads, fc1, conv3, conv2, conv1;
+};
+PartialSizes partial_sizes(const ba3c_handle* h, int B) {
   const int F = h->cfg.fc_neurons;
-  size_t mx = 0;
-  auto upd = [&](const WgradPlan& w) { mx = std::max(mx, (size_t)w.S * w.M * w.N); };
-  upd(plan_wgrad(800, 32, B * 1296, 128, 32));
-  upd(plan_wgrad(800, 64, B * 196, 128, 64));
-  upd(plan_wgrad(576, 64, B * 25, 128, 64));
-  upd(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
-  upd(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
-  mx = std::max(mx, (size_t)WG_P1 * GWg1::M * 32);
-  mx = std::max(mx, (size_t)WG_P2 * GWg2::M * 64);
-  mx = std::max(mx, (size_t)W6_P1 * Lay<3>::W1::M * Lay<3>::W1::COUT);
-  mx = std::max(mx, (size_t)W6_P2 * Lay<3>::W2::M * Lay<3>::W2::COUT);
-  return mx;
+  auto sz = [](const WgradPlan& w) { return (size_t)w.S * w.M * w.N; };
+  PartialSizes p;
+  p.heads = sz(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
+  p.fc1 = sz(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
+  p.conv3 = sz(plan_wgrad(576, 64, B * 25, 128, 64));
+  p.conv2 = std::max({sz(plan_wgrad(800, 64, B * 196, 128, 64)), (size_t)WG_P2 * GWg2::M * 64,
+                      (size_t)W6_P2 * Lay<3>::W2::M * Lay<3>::W2::COUT});
+  p.conv1 = std::max({sz(plan_wgrad(800, 32, B * 1296, 128, 32)), (size_t)WG_P1 * GWg1::M * 32,
+                      (size_t)W6_P1 * Lay<3>::W1::M * Lay<3>::W1::COUT});
+  return p;
 }
 
 Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
@@ -265,7 +273,12 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
     w.dp0 = (float*)take(Bz * P0 * 4);
     w.dzv = (float*)take(Bz * MAXA * 4);
     w.terms = (float*)take(Bz * NTERMS * 4);
-    w.part = (float*)take(max_partials(h, B) * 4);
+    const PartialSizes ps = partial_sizes(h, B);
+    w.part_h = (float*)take(ps.heads * 4);
+    w.part_f = (float*)take(ps.fc1 * 4);
+    w.part_3 = (float*)take(ps.conv3 * 4);
+    w.part_2 = (float*)take(ps.conv2 * 4);
+    w.part_1 = (float*)take(ps.conv1 * 4);
     w.part0 = (float*)take(max_partials0(h, B) * 4);
   }
   w.bytes = off;
@@ -307,6 +320,17 @@ int launch_gemm(ba3c_handle* h, hipStream_t s, int kid, const P& p, int splits) 
 }
 
 int launch_reduce(ba3c_handle* h, hipStream_t s, const float* part, int S, const ReduceMap& mp) {
+  if (h->defer_reduce) {
+    ReduceJobs& j = h->rjobs;
+    if (j.n >= MAX_RJOBS) return fail(BA3C_ERR_INVALID, "too many deferred reductions");
+    j.part[j.n] = part;
+    j.S[j.n] = S;
+    j.mp[j.n] = mp;
+    const int no = mp.kind == 0 ? (mp.M / mp.cin) * mp.cinpad * mp.N : mp.M * mp.N;
+    j.blk0[j.n + 1] = j.blk0[j.n] + (no + 63) / 64;
+    ++j.n;
+    return BA3C_OK;
+  }
   const int MN = mp.M * mp.N;
   {
     ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
@@ -597,12 +621,23 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     return BA3C_OK;
   };
   if (h->side) ws = h->side;   // joins a graph capture of `s` through the fork events
+  // every weight-gradient reduction is deferred into one launch at the end (RAII: an early
+  // error return leaves the handle in immediate mode)
+  struct DeferGuard {
+    ba3c_handle* h;
+    explicit DeferGuard(ba3c_handle* h_) : h(h_) {
+      h->defer_reduce = true;
+      h->rjobs.n = 0;
+      h->rjobs.blk0[0] = 0;
+    }
+    ~DeferGuard() { h->defer_reduce = false; }
+  } defer_guard(h);
   CHECK(fork());
 
   // heads: d fc-pi/W, fc-pi/b, fc-v/W, fc-v/b  (X = h, G = [dz | dV])
   {
     WgradPlan pl = plan_wgrad(F + 1, A + 1, B, 128, 32);
-    BatchWgrad g{w.h, w.dzv, w.part, F, MAXA, 1, pl.M, pl.N, pl.K, pl.kchunk};
+    BatchWgrad g{w.h, w.dzv, w.part_h, F, MAXA, 1, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_HEAD_WGRAD, g, pl.S)));
     ReduceMap mp{};
     mp.kind = 2;
@@ -613,12 +648,12 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.dst_pib = grads + h->tensors[h->idx_pib].offset;
     mp.dst_vW = grads + h->tensors[h->idx_vW].offset;
     mp.dst_vb = grads + h->tensors[h->idx_vb].offset;
-    CHECK(launch_reduce(h, ws, w.part, pl.S, mp));
+    CHECK(launch_reduce(h, ws, w.part_h, pl.S, mp));
   }
   // fc1 weight (+ legacy bias) gradient
   {
     WgradPlan pl = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
-    BatchWgrad g{w.a3, w.dh, w.part, 1600, F, legacy ? 1 : 0, pl.M, pl.N, pl.K, pl.kchunk};
+    BatchWgrad g{w.a3, w.dh, w.part_f, 1600, F, legacy ? 1 : 0, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 64, 2, 2>(h, ws, BA3C_K_FC1_WGRAD, g, pl.S)));
     ReduceMap mp{};
     mp.kind = 1;
@@ -627,7 +662,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.per = h->per;
     mp.wstride = h->wstride;
     mp.dst = grads + h->tensors[h->idx_fc1].offset;
-    CHECK(launch_reduce(h, ws, w.part, pl.S, mp));
+    CHECK(launch_reduce(h, ws, w.part_f, pl.S, mp));
   }
   // fc1 input gradient -> dY3 (ReluGrad of conv3 fused)
   {
@@ -635,7 +670,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
     CHECK(fork());
   }
-  auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad) {
+  auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad, const float* part) {
     ReduceMap mp{};
     mp.kind = 0;
     mp.M = pl.M;
@@ -643,14 +678,14 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.cin = cin;
     mp.cinpad = cinpad;
     mp.dst = grads + h->tensors[h->idx_conv[layer]].offset;
-    return launch_reduce(h, ws, w.part, pl.S, mp);
+    return launch_reduce(h, ws, part, pl.S, mp);
   };
   // conv3
   {
     WgradPlan pl = plan_wgrad(576, 64, B * 25, 128, 64);
-    ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+    ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
-    CHECK(conv_reduce(pl, 3, 64, 64));
+    CHECK(conv_reduce(pl, 3, 64, 64, w.part_3));
     ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0,
                                            NS == 2 ? w.am(AM_DP2, h) : nullptr};
     CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
@@ -660,16 +695,16 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   {
     if (h->band && h->w6) {
       CHECK(launch_wgrad6<typename LY::W2>(h, ws, BA3C_K_CONV2_WGRAD,
-                                          Wg6Args{w.p1, w.dp2, w.c2, w.part, B, w.am(AM_P1, h), w.am(AM_DP2, h)},
+                                          Wg6Args{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)},
                                           W6_P2, grads + h->tensors[h->idx_conv[2]].offset));
     } else if (h->band) {
-      CHECK(launch_wgband<GWg2>(h, ws, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part, B}, WG_P2,
+      CHECK(launch_wgband<GWg2>(h, ws, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part_2, B}, WG_P2,
                                 grads + h->tensors[h->idx_conv[2]].offset, 32));
     } else {
       WgradPlan pl = plan_wgrad(800, 64, B * 196, 128, 64);
-      ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+      ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part_2, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
       CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV2_WGRAD, g, pl.S)));
-      CHECK(conv_reduce(pl, 2, 32, 32));
+      CHECK(conv_reduce(pl, 2, 32, 32, w.part_2));
     }
     if (h->band) {
       const BandArgs ba{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B};
@@ -688,16 +723,16 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   {
     if (h->band && h->w6) {
       CHECK(launch_wgrad6<typename LY::W1>(h, ws, BA3C_K_CONV1_WGRAD,
-                                          Wg6Args{w.p0, w.dp1, w.c1, w.part, B, w.am(AM_P0, h), w.am(AM_DP1, h)},
+                                          Wg6Args{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)},
                                           W6_P1, grads + h->tensors[h->idx_conv[1]].offset));
     } else if (h->band) {
-      CHECK(launch_wgband<GWg1>(h, ws, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part, B}, WG_P1,
+      CHECK(launch_wgband<GWg1>(h, ws, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part_1, B}, WG_P1,
                                 grads + h->tensors[h->idx_conv[1]].offset, 32));
     } else {
       WgradPlan pl = plan_wgrad(800, 32, B * 1296, 128, 32);
-      ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+      ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part_1, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
       CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_CONV1_WGRAD, g, pl.S)));
-      CHECK(conv_reduce(pl, 1, 32, 32));
+      CHECK(conv_reduce(pl, 1, 32, 32, w.part_1));
     }
     if (h->band) {
       const BandArgs ba{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B};
@@ -745,6 +780,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     HIP_TRY(hipEventRecord(h->ev_join, ws));
     HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
   }
+  // all weight-gradient reductions: one launch, every gradient element written once
+  {
+    const ReduceJobs& jb = h->rjobs;
+    ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
+    hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(256), 0, s, jb);
+  }
+  HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
 
@@ -972,7 +1014,8 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
   hipStream_t s = static_cast<hipStream_t>(stream);
   CHECK(ensure_side_stream(h, s));
   Workspace w = carve(h, workspace, batch, true);
-  HIP_TRY(hipMemsetAsync(grads, 0, (size_t)h->flat * 4, s));
+  // no memset of `grads`: the backward pass's single reduction launch writes every element
+  // of every tensor (incl. conv0's zero-padded channels)
   // on the band + split path the weight-prep launch zeroes the ReLU counters
   if (!(h->band && h->b6)) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_SLOTS * 8, s));
   int r = h->cfg.channels == 4 ? (h->ns == 2 ? run_forward<4, 2>(h, s, params, state, batch, w, true)

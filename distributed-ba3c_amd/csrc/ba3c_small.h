@@ -282,6 +282,63 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// All weight-gradient reductions of one backward pass in ONE launch (one job per layer, each
+// with its own partial slabs).  Block b belongs to the job j with blk0[j] <= b < blk0[j+1];
+// per output element the sum runs in the order of wgrad_reduce_kernel (bit-identical).  A
+// conv job's output domain includes the zero-padded input channels (cin <= c < cinpad),
+// written as 0, so with every job in the launch each gradient element is written exactly
+// once and the flat gradient buffer needs no memset.
+constexpr int MAX_RJOBS = 8;
+struct ReduceJobs {
+  int n;
+  const float* part[MAX_RJOBS];
+  int S[MAX_RJOBS];
+  ReduceMap mp[MAX_RJOBS];
+  int blk0[MAX_RJOBS + 1];
+};
+
+__device__ __forceinline__ int reduce_out_size(const ReduceMap& mp) {
+  return mp.kind == 0 ? (mp.M / mp.cin) * mp.cinpad * mp.N : mp.M * mp.N;
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs jobs) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < jobs.n && jobs.blk0[j + 1] <= b) ++j;
+  const ReduceMap& mp = jobs.mp[j];
+  const float* __restrict__ part = jobs.part[j];
+  const int S = jobs.S[j];
+  const int lane = threadIdx.x & 63, zg = threadIdx.x >> 6;
+  const int MN = mp.M * mp.N;
+  const int o = (b - jobs.blk0[j]) * 64 + lane;            // output element of the job
+  const int NO = reduce_out_size(mp);
+  int po = o;                                               // its partial index, -1: padding
+  if (mp.kind == 0 && mp.cinpad != mp.cin && o < NO) {
+    const int n = o % mp.N, r = o / mp.N, kk = r / mp.cinpad, c = r - kk * mp.cinpad;
+    po = c < mp.cin ? (kk * mp.cin + c) * mp.N + n : -1;
+  }
+  float s = 0.f;
+  if (o < NO && po >= 0) {
+    int z = zg;
+    for (; z + 28 < S; z += 32) {
+      float a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = part[(size_t)(z + 4 * u) * MN + po];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += a[u];
+    }
+    for (; z < S; z += 4) s += part[(size_t)z * MN + po];
+  }
+  red[zg][lane] = s;
+  __syncthreads();
+  if (zg == 0 && o < NO) {
+    const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    if (mp.kind == 0) mp.dst[o] = po >= 0 ? v : 0.f;     // [(kk * cinpad + c) * N + n] == o
+    else reduce_store(mp, o / mp.N, o % mp.N, v);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Flat-buffer tensor table and the clip / optimizer kernels (one workgroup per chunk of
 // UPD_CHUNK floats of one tensor).
