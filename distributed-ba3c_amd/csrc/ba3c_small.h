@@ -43,6 +43,15 @@ struct HeadsArgs {
 // p_k (g_k - sum_j p_j g_j) cancels catastrophically when the policy saturates, and fp64 here
 // costs nothing measurable (F*(A+1) FMAs per sample) while keeping the fp32 stored results
 // within rounding of the exact values.
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// One wave per sample; after the dot products lane a < A owns action a, so the softmax /
+// log / gradient run once per lane (one exp and one log per lane instead of MAXA of each,
+// masked, in every lane) with wave reductions for the sums and maxima.
 __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -61,55 +70,29 @@ __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
       if (a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
     accv = fma(hv, (double)p.vW[f], accv);
   }
-  double z[MAXA];
-  double zmax = -INFINITY;
+  const bool mine = lane < A;
+  double z = 0.0;                                   // z[lane] for lane < A
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
     if (a < A) {
-      z[a] = wave_sum_d(acc[a]) + (double)p.pib[a];
-      zmax = fmax(zmax, z[a]);
-    } else {
-      z[a] = 0.0;
+      const double za = wave_sum_d(acc[a]) + (double)p.pib[a];
+      if (lane == a) z = za;
     }
   }
   const double V = wave_sum_d(accv) + (double)p.vb[0];
   // softmax(z)  (tf.nn.softmax: exp(z - max) / sum)
-  double pr[MAXA];
-  double s = 0.0;
-#pragma unroll
-  for (int a = 0; a < MAXA; ++a) {
-    pr[a] = a < A ? exp(z[a] - zmax) : 0.0;
-    s += pr[a];
-  }
-  double pmax = 0.0;
-#pragma unroll
-  for (int a = 0; a < MAXA; ++a) {
-    pr[a] = a < A ? pr[a] / s : 0.0;
-    pmax = fmax(pmax, pr[a]);
-  }
+  const double zmax = wave_max_d(mine ? z : -INFINITY);
+  const double e = mine ? exp(z - zmax) : 0.0;
+  const double pr = e / wave_sum_d(e);              // 0 for lane >= A
+  const double pmax = wave_max_d(pr);
   if (p.probsT) {
-    double zt[MAXA];
-    double ztmax = -INFINITY, st = 0.0;
-    const double ex = (double)p.explore;
-#pragma unroll
-    for (int a = 0; a < MAXA; ++a) {
-      zt[a] = z[a] * ex;
-      if (a < A) ztmax = fmax(ztmax, zt[a]);
-    }
-#pragma unroll
-    for (int a = 0; a < MAXA; ++a) {
-      zt[a] = a < A ? exp(zt[a] - ztmax) : 0.0;
-      st += zt[a];
-    }
-#pragma unroll
-    for (int a = 0; a < MAXA; ++a)
-      if (a < A && lane == a) p.probsT[(size_t)n * A + a] = (float)(zt[a] / st);
+    const double zt = z * (double)p.explore;
+    const double ztmax = wave_max_d(mine ? zt : -INFINITY);
+    const double et = mine ? exp(zt - ztmax) : 0.0;
+    const double st = wave_sum_d(et);
+    if (mine) p.probsT[(size_t)n * A + lane] = (float)(et / st);
   }
-  if (p.probs) {
-#pragma unroll
-    for (int a = 0; a < MAXA; ++a)
-      if (a < A && lane == a) p.probs[(size_t)n * A + a] = (float)pr[a];
-  }
+  if (p.probs && mine) p.probs[(size_t)n * A + lane] = (float)pr;
   if (p.value && lane == 0) p.value[n] = (float)V;
   if (!p.train) return;
 
@@ -117,33 +100,21 @@ __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   const int act = (int)p.action[n];
   const double adv = V - Rn;
   const double beta = (double)p.beta, invB = 1.0 / (double)p.B;
-  double gp[MAXA];
-  double lpa = 0.0, xent = 0.0, sgp = 0.0;
-#pragma unroll
-  for (int a = 0; a < MAXA; ++a) {
-    if (a < A) {
-      const double pe = pr[a] + 1e-6;
-      const double lp = log(pe);
-      xent += pr[a] * lp;
-      if (a == act) lpa = lp;
-      gp[a] = ((a == act ? adv / pe : 0.0) + beta * (lp + pr[a] / pe)) * invB;
-      sgp += gp[a] * pr[a];
-    } else {
-      gp[a] = 0.0;
-    }
-  }
-  double dz[MAXA];
-#pragma unroll
-  for (int a = 0; a < MAXA; ++a) dz[a] = a < A ? pr[a] * (gp[a] - sgp) : 0.0;
+  const double pe = pr + 1e-6;
+  const double lp = mine ? log(pe) : 0.0;
+  const double xent = wave_sum_d(pr * lp);
+  const double lpa = __shfl(lp, act, 64);
+  const double gp = mine ? ((lane == act ? adv / pe : 0.0) + beta * (lp + pr / pe)) * invB : 0.0;
+  const double sgp = wave_sum_d(gp * pr);
+  const double dz = mine ? pr * (gp - sgp) : 0.0;
   const double dV = (V - Rn) * invB;
   // [dz | dV | 0...] row for the head weight-gradient product
-  {
-    double mine = 0.0;
+  if (lane < MAXA) p.dzv[(size_t)n * MAXA + lane] = (float)(lane == A ? dV : dz);
+  double dza[MAXA];
 #pragma unroll
-    for (int a = 0; a < MAXA; ++a)
-      if (lane == a) mine = dz[a];
-    if (lane == A) mine = dV;
-    if (lane < MAXA) p.dzv[(size_t)n * MAXA + lane] = (float)mine;
+  for (int a = 0; a < MAXA; ++a) {
+    dza[a] = 0.0;
+    if (a < A) dza[a] = __shfl(dz, a, 64);          // uniform branch: A broadcasts only
   }
   float* dhn = p.dh + (size_t)n * p.F;
   for (int f = lane; f < p.F; f += 64) {
@@ -151,7 +122,7 @@ __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
     double g = dV * (double)p.vW[f];
 #pragma unroll
     for (int a = 0; a < MAXA; ++a)
-      if (a < A) g = fma(dz[a], (double)wr[a], g);
+      if (a < A) g = fma(dza[a], (double)wr[a], g);
     if (p.legacy && !(hn[f] > 0.f)) g = 0.0;
     dhn[f] = (float)g;
   }
