@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
   __shared__ float red4[4];
   if (y == 0) {
     if (a.relu)
-      for (int i = blockIdx.x * 256 + threadIdx.x; i < RELU_SLOTS; i += gridDim.x * 256) a.relu[i] = 0ull;
+      for (int i = blockIdx.x * 256 + threadIdx.x; i < RELU_WORDS; i += gridDim.x * 256) a.relu[i] = 0ull;
     if (a.amax)
       for (int i = blockIdx.x * 256 + threadIdx.x; i < a.n_amax; i += gridDim.x * 256) a.amax[i] = 0u;
   }

@@ -85,11 +85,14 @@ struct ba3c_handle {
   // producer of a split operand to publish its max, so it is used only when all split
   // kernels are on (band, b6, w6, split).
   int ns = 2;
-  // backward weight gradients on a side stream (BA3C_OVERLAP=1; created on the first training
-  // call that is not being captured). Off by default: r01t/u measured +0.5% step throughput
-  // (561k vs 557k samples/s) because conv1's dgrad and wgrad kernels each fill the chip, and
-  // concurrent kernels make the per-kernel durations (roofline, rocprof) meaningless.
-  bool overlap = false;
+  // backward weight gradients on a side stream (created on the first training call that is
+  // not being captured): 0 never (BA3C_OVERLAP=0), 1 always (BA3C_OVERLAP=1), 2 (default) for
+  // batches <= OVERLAP_B only.  Large batches: r01t/u measured +0.5% step throughput (561k vs
+  // 557k samples/s) because conv1's dgrad and wgrad kernels each fill the chip, and concurrent
+  // kernels make the per-kernel durations (roofline, rocprof) meaningless.  Small batches: each
+  // backward kernel is a few latency-bound workgroups, so the weight-gradient chain runs in
+  // the input-gradient chain's shadow.
+  int overlap = 2;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -124,6 +127,7 @@ using GConv2D = BandGeom<22, 22, 64, 32, 5, 5, 6, false, 1, 8, 4, 4, 7, 7, 14, 1
 //       wave of work.  Every output's K order (phase, tap, channel chunk, product) is the same
 //       in both geometries, so results are bit-identical across the switch.
 constexpr int SMALL_B = 128;
+constexpr int OVERLAP_B = 128;   // default side-stream weight gradients up to this batch
 using GConv2DW = BandGeom<22, 22, 64, 32, 5, 5, 18, false, 1, 8, 4, 4, 7, 7, 14, 14>;
 using GConv2FS = BandGeom<18, 18, 32, 64, 5, 5, 2, true, 0, 4>;
 using GConv2DS = BandGeom<22, 22, 64, 32, 5, 5, 3, false, 1, 8, 4, 4, 7, 7, 14, 14>;
@@ -259,7 +263,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   w.a3 = (float*)take(Bz * A3 * 4);
   w.h = (float*)take(Bz * F * 4);
   w.fcpart = (float*)take((size_t)FC_SPLIT * Bz * F * 4);
-  w.relu = (unsigned long long*)take(RELU_SLOTS * 8);
+  w.relu = (unsigned long long*)take(RELU_WORDS * 8);
   w.wt = (float*)take((size_t)WT_TOTAL * 4);
   w.wt6 = (uint16_t*)take((size_t)3 * WT_C0F * 2);
   if (train) {
@@ -310,7 +314,11 @@ int launch_gemm(ba3c_handle* h, hipStream_t s, int kid, const P& p, int splits) 
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
   {
     ProbeScope ps(h, s, kid);
-    if (h->g6)
+    // fewer workgroups than CUs: each walks its K latency-bound, so keep 4 k-tiles in flight
+    const bool deep = (int)(grid.x * grid.y * grid.z) < h->cus;
+    if (h->g6 && deep)
+      hipLaunchKernelGGL((gemm6_kernel<BM, BN, WGM, WGN, P, 4>), grid, dim3(GEMM_THREADS), 0, s, p);
+    else if (h->g6)
       hipLaunchKernelGGL((gemm6_kernel<BM, BN, WGM, WGN, P>), grid, dim3(GEMM_THREADS), 0, s, p);
     else
       hipLaunchKernelGGL((gemm_kernel<BM, BN, WGM, WGN, P>), grid, dim3(GEMM_THREADS), 0, s, p);
@@ -568,18 +576,19 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
   CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
   // split-K: K = 1600 in FC_SPLIT fixed chunks (a 128x64 tile over all of K is one
-  // workgroup's 50 serial k-tiles: latency-bound at any batch), then one finishing pass
+  // workgroup's 50 serial k-tiles: latency-bound at any batch); the chunk sums (+ legacy bias,
+  // ReLU, count) are finished inside the heads kernel (run_heads), which reads them anyway
   FcFwd fc{w.a3, prm + h->tensors[h->idx_fc1].offset, w.h, rc, h->per, h->wstride,
            h->cfg.replace_with_conv ? 0 : 1, B, F, 1600, FC_KCHUNK, w.fcpart};
   {
     ProbeScope ps(h, s, BA3C_K_FC1_FWD);
     const dim3 grid((B + 127) / 128, (F + 63) / 64, FC_SPLIT);
-    if (h->g6)
+    if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
+      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, 4>), grid, dim3(GEMM_THREADS), 0, s, fc);
+    else if (h->g6)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);
     else
       hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);
-    const int nblk = (int)std::min<size_t>(((size_t)B * F + 255) / 256, 2048);
-    hipLaunchKernelGGL(fc_finish_kernel, dim3(nblk), dim3(256), 0, s, fc, FC_SPLIT);
   }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
@@ -588,7 +597,7 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
 // Create the side stream + fork/join events on the first training call made outside a
 // graph capture (stream creation is not a capturable operation).
 int ensure_side_stream(ba3c_handle* h, hipStream_t s) {
-  if (!h->overlap || h->side) return BA3C_OK;
+  if (h->overlap == 0 || h->side) return BA3C_OK;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(s, &cs));
   if (cs != hipStreamCaptureStatusNone) return BA3C_OK;
@@ -620,7 +629,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ++nfork;
     return BA3C_OK;
   };
-  if (h->side) ws = h->side;   // joins a graph capture of `s` through the fork events
+  // the side stream joins a graph capture of `s` through the fork events
+  if (h->side && (h->overlap == 1 || B <= OVERLAP_B)) ws = h->side;
   // every weight-gradient reduction is deferred into one launch at the end (RAII: an early
   // error return leaves the handle in immediate mode)
   struct DeferGuard {
@@ -792,8 +802,20 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
 
 int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, int B,
               const int64_t* action, const float* R, float beta, float explore, bool train,
-              float* probs, float* probsT, float* value) {
+              float* probs, float* probsT, float* value, double* scalars = nullptr) {
   HeadsArgs a{};
+  a.fcpart = w.fcpart;
+  a.fc_split = FC_SPLIT;
+  a.per = h->per;
+  a.wstride = h->wstride;
+  a.fc_w1 = prm + h->tensors[h->idx_fc1].offset;
+  a.relu_count = train ? w.relu : nullptr;
+  a.done = w.relu + RELU_SLOTS;
+  // the scalar reduction rides on the heads launch (last workgroup) for small batches only:
+  // with B/4 workgroups all finishing together, B > 256 puts hundreds of same-address atomics
+  // and a B-long serial reduction at the kernel's tail (r02f: heads 29 -> 75 us at B=2048)
+  const bool fuse_scalars = train && scalars && B <= 256;
+  a.scalars = fuse_scalars ? scalars : nullptr;
   a.h = w.h;
   a.piW = prm + h->tensors[h->idx_piW].offset;
   a.pib = prm + h->tensors[h->idx_pib].offset;
@@ -820,6 +842,10 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
     hipLaunchKernelGGL(heads_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a);
   }
   HIP_TRY(hipGetLastError());
+  if (train && scalars && !fuse_scalars) {
+    hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, w.terms, B, beta, w.relu, scalars);
+    HIP_TRY(hipGetLastError());
+  }
   return BA3C_OK;
 }
 
@@ -852,7 +878,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = (e[0] == '1');
+  if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
   if (const char* e = getenv("BA3C_PIPE")) h->pipe = (e[0] == '1');
   {
     int dev = 0, n = 0;
@@ -1017,19 +1043,15 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
   // no memset of `grads`: the backward pass's single reduction launch writes every element
   // of every tensor (incl. conv0's zero-padded channels)
   // on the band + split path the weight-prep launch zeroes the ReLU counters
-  if (!(h->band && h->b6)) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_SLOTS * 8, s));
+  if (!(h->band && h->b6)) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_WORDS * 8, s));
   int r = h->cfg.channels == 4 ? (h->ns == 2 ? run_forward<4, 2>(h, s, params, state, batch, w, true)
                                                : run_forward<4, 3>(h, s, params, state, batch, w, true))
                                : (h->ns == 2 ? run_forward<12, 2>(h, s, params, state, batch, w, true)
                                              : run_forward<12, 3>(h, s, params, state, batch, w, true));
   if (r != BA3C_OK) return r;
+  // heads + loss + its gradient, fc1's split-K finish and (last workgroup) the TfDictOp scalars
   CHECK(run_heads(h, s, params, w, batch, action, futurereward, entropy_beta, 1.0f, true, nullptr,
-                  nullptr, nullptr));
-  if (scalars) {
-    hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, w.terms, batch, entropy_beta,
-                       w.relu, scalars);
-    HIP_TRY(hipGetLastError());
-  }
+                  nullptr, nullptr, scalars));
   if (h->cfg.channels == 4)
     return h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads)
                       : run_backward<4, 3>(h, s, params, state, batch, w, grads);

@@ -23,6 +23,51 @@ namespace ba3c {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int GEMM_BK = 32;
+
+__device__ __forceinline__ float4 u8x4_to_f4(uint32_t v) {
+  return make_float4((float)(v & 255u), (float)((v >> 8) & 255u), (float)((v >> 16) & 255u),
+                     (float)(v >> 24));
+}
+
+// Operand fetches are branch-free and return the RAW loaded words; `fin` turns them into the
+// float4 operand when the k-tile is staged.  An out-of-range element is fetched from a
+// 16-byte zero block instead of its tensor (no select on the data), so nothing consumes a
+// load before it is staged: a load under a branch, or an op on its result right after it,
+// makes the compiler drain every outstanding load (vmcnt(0)) there, which would serialise
+// the k-tile register ring of gemm6_kernel.
+__device__ __attribute__((aligned(16))) float kZero4[4] = {0.f, 0.f, 0.f, 0.f};
+__device__ __attribute__((aligned(16))) float kOne4[4] = {1.f, 0.f, 0.f, 0.f};
+
+__device__ __forceinline__ float4 ld4(const float* p, bool ok) {
+  return *reinterpret_cast<const float4*>(ok ? p : kZero4);
+}
+__device__ __forceinline__ uint32_t ld_u8x4(const uint8_t* p, bool ok) {
+  return *reinterpret_cast<const uint32_t*>(ok ? p : reinterpret_cast<const uint8_t*>(kZero4));
+}
+struct UnpoolRaw {
+  float4 g;
+  uint32_t cd, sub;
+};
+// pin(): an empty volatile asm that "redefines" the raw words where a k-tile is staged, so
+// no pass can hoist the staging arithmetic of a later tile (and the wait for its loads)
+// ahead of the current one
+__device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ void pin(uint32_t& u) { asm volatile("" : "+v"(u)); }
+__device__ __forceinline__ float4 fin(const float4& v) { return v; }
+__device__ __forceinline__ float4 fin(uint32_t u) { return u8x4_to_f4(u); }
+__device__ __forceinline__ void pin(UnpoolRaw& r) {
+  pin(r.g);
+  asm volatile("" : "+v"(r.cd), "+v"(r.sub));
+}
+__device__ __forceinline__ float4 fin(const UnpoolRaw& r) {
+  float4 g = r.g;
+  g.x = ((r.cd & 255u) == r.sub) ? g.x : 0.f;
+  g.y = (((r.cd >> 8) & 255u) == r.sub) ? g.y : 0.f;
+  g.z = (((r.cd >> 16) & 255u) == r.sub) ? g.z : 0.f;
+  g.w = ((r.cd >> 24) == r.sub) ? g.w : 0.f;
+  return g;
+}
+
 constexpr int GEMM_THREADS = 256;
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
@@ -85,16 +130,16 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_kernel(const P p) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       if constexpr (P::A_KCONTIG)
-        ra[i] = p.a_load(arow[i], k0 + (tid & 7) * 4, kend);
+        ra[i] = fin(p.a_load(arow[i], k0 + (tid & 7) * 4, kend));
       else
-        ra[i] = p.a_load_t(arow[0], k0 + tid / QA + RA * i, kend);
+        ra[i] = fin(p.a_load_t(arow[0], k0 + tid / QA + RA * i, kend));
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (P::B_KCONTIG)
-        rb[i] = p.b_load(brow[i], k0 + (tid & 7) * 4, kend);
+        rb[i] = fin(p.b_load(brow[i], k0 + (tid & 7) * 4, kend));
       else
-        rb[i] = p.b_load_t(brow[0], k0 + tid / QB + RB * i, kend);
+        rb[i] = fin(p.b_load_t(brow[0], k0 + tid / QB + RB * i, kend));
     }
   };
   auto store = [&]() {

@@ -29,11 +29,15 @@ namespace ba3c {
 
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 
-constexpr int G6_RP = GEMM_BK * 2 + 16;   // row pitch (bytes) of a k-contiguous plane
+constexpr int G6_RP = GEMM_BK * 2 + 16;
+  // row pitch (bytes) of a k-contiguous plane
 // K-row pitch of a transposed plane of `rows` operand rows: 64 or 192 mod 256 bytes
 constexpr int tr_pitch(int rows) { return rows * 2 + (64 - (rows * 2) % 128 + 128) % 128; }
 
-template <int BM, int BN, int WGM, int WGN, class P>
+// G6_DEPTH: k-tiles in flight per thread (register ring); 2 = classic one-ahead prefetch.
+// Small-batch launches (a few workgroups walking a long K each) take 4, large ones 2 (the
+// deeper ring's registers cost occupancy that the big launches need more).
+template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2>
 __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
   static_assert(WGM * WGN == 4, "4 waves per workgroup");
   constexpr int BK = GEMM_BK;
@@ -81,21 +85,26 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
     brow[0] = p.b_col(n0 + (tid % QB) * 4);
   }
 
-  float4 ra[NA], rb[NB];
-  auto load = [&](int k0) {
+  // register ring of G6_DEPTH k-tiles: the loads of tile t + G6_DEPTH - 1 are issued before
+  // tile t is staged, so G6_DEPTH - 1 tiles of global-load latency overlap the MFMA loop (the
+  // small-batch launches have a few workgroups each walking a long K: one exposed load round
+  // trip per k-tile was their whole time).  Stage indices are compile-time after unrolling.
+  typename P::ARaw ra[G6_DEPTH][NA];
+  typename P::BRaw rb[G6_DEPTH][NB];
+  auto load = [&](int st, int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       if constexpr (P::A_KCONTIG)
-        ra[i] = p.a_load(arow[i], k0 + (tid & 7) * 4, kend);
+        ra[st][i] = p.a_load(arow[i], k0 + (tid & 7) * 4, kend);
       else
-        ra[i] = p.a_load_t(arow[0], k0 + tid / QA + RA * i, kend);
+        ra[st][i] = p.a_load_t(arow[0], k0 + tid / QA + RA * i, kend);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (P::B_KCONTIG)
-        rb[i] = p.b_load(brow[i], k0 + (tid & 7) * 4, kend);
+        rb[st][i] = p.b_load(brow[i], k0 + (tid & 7) * 4, kend);
       else
-        rb[i] = p.b_load_t(brow[0], k0 + tid / QB + RB * i, kend);
+        rb[st][i] = p.b_load_t(brow[0], k0 + tid / QB + RB * i, kend);
     }
   };
   // split a float4 into 3 planes and store it (8 bytes per plane): KC -> 4 K of row r at
@@ -110,20 +119,26 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
     for (int s = 0; s < 3; ++s)
       *reinterpret_cast<uint2*>(base + s * plane_bytes + off) = make_uint2(hs[s][0], hs[s][1]);
   };
-  auto store = [&]() {
+  auto store = [&](int st) {
+    if constexpr (G6_DEPTH > 2) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) pin(ra[st][i]);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) pin(rb[st][i]);
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       if constexpr (P::A_KCONTIG)
-        put(As, PA, true, TPA, (tid >> 3) + 32 * i, (tid & 7) * 4, ra[i]);
+        put(As, PA, true, TPA, (tid >> 3) + 32 * i, (tid & 7) * 4, fin(ra[st][i]));
       else
-        put(As, PA, false, TPA, (tid % QA) * 4, tid / QA + RA * i, ra[i]);
+        put(As, PA, false, TPA, (tid % QA) * 4, tid / QA + RA * i, fin(ra[st][i]));
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (P::B_KCONTIG)
-        put(Bs, PB, true, TPB, (tid >> 3) + 32 * i, (tid & 7) * 4, rb[i]);
+        put(Bs, PB, true, TPB, (tid >> 3) + 32 * i, (tid & 7) * 4, fin(rb[st][i]));
       else
-        put(Bs, PB, false, TPB, (tid % QB) * 4, tid / QB + RB * i, rb[i]);
+        put(Bs, PB, false, TPB, (tid % QB) * 4, tid / QB + RB * i, fin(rb[st][i]));
     }
   };
 
@@ -153,11 +168,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
     return __builtin_bit_cast(bf16x8v, u32x4{u0.x, u0.y, u1.x, u1.y});
   };
 
-  if (kbeg < kend) load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    store();
-    __syncthreads();
-    if (k0 + BK < kend) load(k0 + BK);
+  auto tile = [&](int k0) {
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8v av[3][TM], bv[3][TN];
@@ -178,7 +189,38 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
           for (int b = 0; b < TN; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[PA_[pr]][a], bv[PB_[pr]][b], acc[a][b], 0, 0, 0);
     }
-    __syncthreads();
+  };
+
+  // Prologue loads and the steady-state prefetches are unconditional (a tile past kend reads
+  // the zero block): a conditionally issued load leaves the compiler unsure how many loads are
+  // outstanding where the paths join, and it then waits for all of them.  Full groups of
+  // G6_DEPTH tiles (the last may be partial: its loads mask k >= kend) run branch-free; the
+  // < G6_DEPTH tail tiles are already in the ring.
+#pragma unroll
+  for (int st = 0; st < G6_DEPTH - 1; ++st) load(st, kbeg + st * BK);
+  int kk = kbeg;
+  for (; kk + (G6_DEPTH - 1) * BK < kend; kk += G6_DEPTH * BK) {   // >= G6_DEPTH tiles left
+#pragma unroll
+    for (int st = 0; st < G6_DEPTH; ++st) {
+      // sched barriers: the split arithmetic of a later stage would otherwise be hoisted to
+      // the top of the group, waiting for loads that are meant to stay in flight
+      __builtin_amdgcn_sched_barrier(0);
+      load((st + G6_DEPTH - 1) % G6_DEPTH, kk + (st + G6_DEPTH - 1) * BK);
+      store(st);
+      __syncthreads();
+      tile(kk + st * BK);
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int st = 0; st < G6_DEPTH - 1; ++st) {
+    if (kk + st * BK < kend) {                 // uniform
+      store(st);
+      __syncthreads();
+      tile(kk + st * BK);
+      __syncthreads();
+    }
   }
 
   p.template epilogue<TM, TN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, blockIdx.z);

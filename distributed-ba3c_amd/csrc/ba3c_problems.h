@@ -7,19 +7,20 @@
 // gradient is zero).  Backward loaders "unpool" on the fly from (dP, code), so no
 // full-resolution gradient map is ever written.
 #pragma once
+#include <type_traits>
+
 #include "ba3c_gemm.h"
 
 namespace ba3c {
 
-__device__ __forceinline__ float4 u8x4_to_f4(uint32_t v) {
-  return make_float4((float)(v & 255u), (float)((v >> 8) & 255u), (float)((v >> 16) & 255u),
-                     (float)(v >> 24));
-}
 
 // count_nonzero of ReLU outputs (train.py:271): one integer add per wave, spread over
 // RELU_SLOTS counters so 10^5 waves do not serialise on one address (summed by the scalars
 // kernel; integer adds are exact in any order).
 constexpr int RELU_SLOTS = 1024;
+// the ReLU-count region holds one more word: the heads kernel's completion counter (its last
+// workgroup reduces the per-sample loss terms), zeroed with the counters every training step
+constexpr int RELU_WORDS = RELU_SLOTS + 1;
 __device__ __forceinline__ void relu_count_add(unsigned long long* slots, unsigned long long pos, int lane) {
   pos = wave_sum_u64(pos);
   if (lane == 0 && pos) {
@@ -68,19 +69,16 @@ __device__ __forceinline__ uint32_t amax_all(const uint32_t* slots, int B, uint3
   return r;
 }
 
-// dY at conv-output position (y, x) from pooled grad dP and argmax codes.
+// dY at conv-output position (y, x) from pooled grad dP and argmax codes (0 where !ok).
 template <int PW, int COUT>
-__device__ __forceinline__ float4 unpool4(const float* __restrict__ dP, const uint8_t* __restrict__ code,
-                                          int n_ph_base, int y, int x, int c) {
-  const int pidx = n_ph_base + (y >> 1) * PW + (x >> 1);
-  const uint32_t sub = ((y & 1) << 1) | (x & 1);
-  float4 g = *reinterpret_cast<const float4*>(dP + (size_t)pidx * COUT + c);
-  const uint32_t cd = *reinterpret_cast<const uint32_t*>(code + (size_t)pidx * COUT + c);
-  g.x = ((cd & 255u) == sub) ? g.x : 0.f;
-  g.y = (((cd >> 8) & 255u) == sub) ? g.y : 0.f;
-  g.z = (((cd >> 16) & 255u) == sub) ? g.z : 0.f;
-  g.w = ((cd >> 24) == sub) ? g.w : 0.f;
-  return g;
+__device__ __forceinline__ UnpoolRaw unpool4(const float* __restrict__ dP, const uint8_t* __restrict__ code,
+                                             int n_ph_base, int y, int x, int c, bool ok = true) {
+  const size_t e = (size_t)(n_ph_base + (y >> 1) * PW + (x >> 1)) * COUT + c;
+  UnpoolRaw r;
+  r.g = ld4(dP + e, ok);
+  r.cd = ld_u8x4(code + e, ok);
+  r.sub = ok ? ((y & 1) << 1) | (x & 1) : 256u;   // 256: matches no code
+  return r;
 }
 
 // ------------------------------------------------------------------------------------
@@ -98,6 +96,8 @@ struct ConvFwd {
   static constexpr int KDIM = KH * KW * CIN;
   using ARow = int;
   using BRow = int;
+  using ARaw = typename std::conditional<SRC_U8, uint32_t, float4>::type;
+  using BRaw = float4;
   const void* src;
   const float* w;
   float* out;
@@ -125,24 +125,24 @@ struct ConvFwd {
     }
     return ((n * HIN + oh) * WIN + ow) * CIN;
   }
-  __device__ float4 a_load(int row, int k, int kend) const {
-    if (row < 0 || k >= kend) return f4zero();
+  __device__ ARaw a_load(int row, int k, int kend) const {
+    const bool ok = row >= 0 && k < kend;
     const int kh = k / (KW * CIN);
     const int r = k - kh * (KW * CIN);
     const int kw = r / CIN, c = r - kw * CIN;
     const int off = row + (kh * WIN + kw) * CIN + c;
     if constexpr (SRC_U8)
-      return u8x4_to_f4(*reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(src) + off));
+      return ld_u8x4(static_cast<const uint8_t*>(src) + off, ok);
     else
-      return *reinterpret_cast<const float4*>(static_cast<const float*>(src) + off);
+      return ld4(static_cast<const float*>(src) + off, ok);
   }
   __device__ int b_col(int n) const { return n < N ? n : -1; }
-  __device__ float4 b_load_t(int ncol, int k, int kend) const {
-    if (ncol < 0 || k >= kend) return f4zero();
+  __device__ BRaw b_load_t(int ncol, int k, int kend) const {
+    const bool ok = ncol >= 0 && k < kend;
     const int kh = k / (KW * CIN);
     const int r = k - kh * (KW * CIN);
     const int kw = r / CIN, c = r - kw * CIN;
-    return *reinterpret_cast<const float4*>(w + ((kh * KW + kw) * CINPAD + c) * COUT + ncol);
+    return ld4(w + ((kh * KW + kw) * CINPAD + c) * COUT + ncol, ok);
   }
   template <int TM, int TN>
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
@@ -207,6 +207,8 @@ struct ConvDgrad {
   static constexpr int HO = HIN - KH + 1, WO = WIN - KW + 1, PH = HO / 2, PW = WO / 2;
   struct ARow { int n, y, x; };
   using BRow = int;
+  using ARaw = typename std::conditional<POOLED, UnpoolRaw, float4>::type;
+  using BRaw = float4;
   const float* dy;       // POOLED: dP [B,PH,PW,COUT]  else dY [B,HO,WO,COUT]
   const uint8_t* code;   // POOLED only
   const float* w;        // [KH,KW,CIN,COUT]
@@ -223,25 +225,24 @@ struct ConvDgrad {
     r.x = q - r.y * WIN;
     return r;
   }
-  __device__ float4 a_load(const ARow& r, int k, int kend) const {
-    if (r.n < 0 || k >= kend) return f4zero();
+  __device__ ARaw a_load(const ARow& r, int k, int kend) const {
     const int kh = k / (KW * COUT);
     const int q = k - kh * (KW * COUT);
     const int kw = q / COUT, o = q - kw * COUT;
     const int yy = r.y - kh, xx = r.x - kw;
-    if (yy < 0 || yy >= HO || xx < 0 || xx >= WO) return f4zero();
+    const bool ok = r.n >= 0 && k < kend && yy >= 0 && yy < HO && xx >= 0 && xx < WO;
     if constexpr (POOLED)
-      return unpool4<PW, COUT>(dy, code, r.n * (PH * PW), yy, xx, o);
+      return unpool4<PW, COUT>(dy, code, r.n * (PH * PW), yy, xx, o, ok);
     else
-      return *reinterpret_cast<const float4*>(dy + ((size_t)(r.n * HO + yy) * WO + xx) * COUT + o);
+      return ld4(dy + ((size_t)(r.n * HO + yy) * WO + xx) * COUT + o, ok);
   }
   __device__ int b_row(int n) const { return n < N ? n : -1; }
-  __device__ float4 b_load(int ci, int k, int kend) const {
-    if (ci < 0 || k >= kend) return f4zero();
+  __device__ BRaw b_load(int ci, int k, int kend) const {
+    const bool ok = ci >= 0 && k < kend;
     const int kh = k / (KW * COUT);
     const int q = k - kh * (KW * COUT);
     const int kw = q / COUT, o = q - kw * COUT;
-    return *reinterpret_cast<const float4*>(w + ((kh * KW + kw) * CIN + ci) * COUT + o);
+    return ld4(w + ((kh * KW + kw) * CIN + ci) * COUT + o, ok);
   }
   template <int TM, int TN>
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
@@ -283,6 +284,8 @@ struct ConvWgrad {
   static constexpr int HO = HIN - KH + 1, WO = WIN - KW + 1, PH = HO / 2, PW = WO / 2;
   using ARow = int;
   using BRow = int;
+  using ARaw = typename std::conditional<SRC_U8, uint32_t, float4>::type;
+  using BRaw = typename std::conditional<POOLED, UnpoolRaw, float4>::type;
   const void* src;       // X [B,HIN,WIN,CIN] (u8 or f32)
   const float* dy;       // POOLED: dP [B,PH,PW,COUT] else dY [B,HO,WO,COUT]
   const uint8_t* code;
@@ -297,27 +300,27 @@ struct ConvWgrad {
     const int kw = q / CIN, c = q - kw * CIN;
     return (kh * WIN + kw) * CIN + c;
   }
-  __device__ float4 a_load_t(int mo, int k, int kend) const {
-    if (mo < 0 || k >= kend) return f4zero();
+  __device__ ARaw a_load_t(int mo, int k, int kend) const {
+    const bool ok = mo >= 0 && k < kend;
     const int n = k / (HO * WO);
     const int q = k - n * (HO * WO);
     const int y = q / WO, x = q - y * WO;
     const size_t off = ((size_t)(n * HIN + y) * WIN + x) * CIN + mo;
     if constexpr (SRC_U8)
-      return u8x4_to_f4(*reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(src) + off));
+      return ld_u8x4(static_cast<const uint8_t*>(src) + off, ok);
     else
-      return *reinterpret_cast<const float4*>(static_cast<const float*>(src) + off);
+      return ld4(static_cast<const float*>(src) + off, ok);
   }
   __device__ int b_col(int n) const { return n < N ? n : -1; }
-  __device__ float4 b_load_t(int c, int k, int kend) const {
-    if (c < 0 || k >= kend) return f4zero();
+  __device__ BRaw b_load_t(int c, int k, int kend) const {
+    const bool ok = c >= 0 && k < kend;
     const int n = k / (HO * WO);
     const int q = k - n * (HO * WO);
     const int y = q / WO, x = q - y * WO;
     if constexpr (POOLED)
-      return unpool4<PW, COUT>(dy, code, n * (PH * PW), y, x, c);
+      return unpool4<PW, COUT>(dy, code, n * (PH * PW), y, x, c, ok);
     else
-      return *reinterpret_cast<const float4*>(dy + (size_t)k * COUT + c);
+      return ld4(dy + (size_t)k * COUT + c, ok);
   }
   template <int TM, int TN>
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int z) const {
@@ -346,28 +349,28 @@ struct FcFwd {
   static constexpr bool A_KCONTIG = true, B_KCONTIG = false;
   using ARow = int;
   using BRow = int;
+  using ARaw = float4;
+  using BRaw = float4;
   const float* a3;      // [B,1600]
   const float* w1;      // split 0 base
   float* h;             // [B,F]
   unsigned long long* relu_count;
   int per, wstride, legacy;
   int M, N, K, kchunk;
-  float* part;          // split-K (kchunk > 0): raw partial slabs [z][M][N]; fc_finish_kernel
-                        // sums them in z order and applies the epilogue below
+  float* part;          // split-K (kchunk > 0): raw partial slabs [z][M][N]; the heads kernel
+                        // (ba3c_small.h) sums them in z order and applies the legacy epilogue
 
   __device__ int a_row(int m) const { return m < M ? m * 1600 : -1; }
-  __device__ float4 a_load(int row, int k, int kend) const {
-    if (row < 0 || k >= kend) return f4zero();
-    return *reinterpret_cast<const float4*>(a3 + (size_t)row + k);
+  __device__ ARaw a_load(int row, int k, int kend) const {
+    return ld4(a3 + (size_t)row + k, row >= 0 && k < kend);
   }
   __device__ int b_col(int n) const {
     if (n >= N) return -1;
     const int s = n / per;
     return s * wstride + (n - s * per);
   }
-  __device__ float4 b_load_t(int c, int k, int kend) const {
-    if (c < 0 || k >= kend) return f4zero();
-    return *reinterpret_cast<const float4*>(w1 + c + (size_t)k * per);
+  __device__ BRaw b_load_t(int c, int k, int kend) const {
+    return ld4(w1 + c + (size_t)k * per, c >= 0 && k < kend);
   }
   template <int TM, int TN>
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int z) const {
@@ -413,31 +416,13 @@ struct FcFwd {
   }
 };
 
-// FC1 forward, split-K finish: h[m][n] = epilogue(sum_z part[z][m][n]) with FcFwd's
-// epilogue (legacy: + bias, ReLU, positive count).  The split is fixed (FC_SPLIT chunks of
-// FC_KCHUNK), so every row's summation order — and so its rounding — is the same at any batch.
-__global__ void __launch_bounds__(256) fc_finish_kernel(const FcFwd p, int S) {
-  const int lane = threadIdx.x & 63;
-  const size_t MN = (size_t)p.M * p.N;
-  unsigned long long pos = 0;
-  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < MN; e += (size_t)gridDim.x * 256) {
-    float v = p.part[e];
-    for (int z = 1; z < S; ++z) v += p.part[(size_t)z * MN + e];
-    if (p.legacy) {
-      const int col = (int)(e % p.N), sidx = col / p.per;
-      v = fmaxf(v + p.w1[sidx * p.wstride + 1600 * p.per + (col - sidx * p.per)], 0.f);
-      pos += v > 0.f;
-    }
-    p.h[e] = v;
-  }
-  if (p.legacy && p.relu_count) relu_count_add(p.relu_count, pos, lane);
-}
-
 // FC1 input gradient: dY3[b][j] = (sum_f dh[b][f] W1[j][f]) * (a3[b][j] > 0)
 struct FcDgrad {
   static constexpr bool A_KCONTIG = true, B_KCONTIG = true;
   using ARow = int;
   using BRow = int;
+  using ARaw = float4;
+  using BRaw = float4;
   const float* dh;   // [B,F]
   const float* w1;
   const float* a3;   // [B,1600] relu mask source
@@ -446,15 +431,13 @@ struct FcDgrad {
   int M, N, K, kchunk;  // M=B, N=1600, K=F
 
   __device__ int a_row(int m) const { return m < M ? m * K : -1; }
-  __device__ float4 a_load(int row, int k, int kend) const {
-    if (row < 0 || k >= kend) return f4zero();
-    return *reinterpret_cast<const float4*>(dh + (size_t)row + k);
+  __device__ ARaw a_load(int row, int k, int kend) const {
+    return ld4(dh + (size_t)row + k, row >= 0 && k < kend);
   }
   __device__ int b_row(int n) const { return n < N ? n * per : -1; }
-  __device__ float4 b_load(int row, int k, int kend) const {
-    if (row < 0 || k >= kend) return f4zero();
+  __device__ BRaw b_load(int row, int k, int kend) const {
     const int s = k / per;
-    return *reinterpret_cast<const float4*>(w1 + (size_t)s * wstride + row + (k - s * per));
+    return ld4(w1 + (size_t)s * wstride + row + (k - s * per), row >= 0 && k < kend);
   }
   template <int TM, int TN>
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int) const {
@@ -483,6 +466,8 @@ struct BatchWgrad {
   static constexpr bool A_KCONTIG = false, B_KCONTIG = false;
   using ARow = int;
   using BRow = int;
+  using ARaw = float4;
+  using BRaw = float4;
   const float* x;    // [B, kin]
   const float* g;    // [B, gld]
   float* part;
@@ -494,15 +479,14 @@ struct BatchWgrad {
     if (has_bias && m == kin) return -2;
     return -1;
   }
-  __device__ float4 a_load_t(int c, int k, int kend) const {
-    if (c == -1 || k >= kend) return f4zero();
-    if (c == -2) return make_float4(1.f, 0.f, 0.f, 0.f);
-    return *reinterpret_cast<const float4*>(x + (size_t)k * kin + c);
+  __device__ ARaw a_load_t(int c, int k, int kend) const {
+    // the bias row (c == -2) reads {1, 0, 0, 0}
+    const float* q = (c == -2 && k < kend) ? kOne4 : x + (size_t)k * kin + c;
+    return ld4(q, (c >= 0 || c == -2) && k < kend);
   }
   __device__ int b_col(int n) const { return n < N ? n : -1; }
-  __device__ float4 b_load_t(int c, int k, int kend) const {
-    if (c < 0 || k >= kend) return f4zero();
-    return *reinterpret_cast<const float4*>(g + (size_t)k * gld + c);
+  __device__ BRaw b_load_t(int c, int k, int kend) const {
+    return ld4(g + (size_t)k * gld + c, c >= 0 && k < kend);
   }
   template <int TM, int TN>
   __device__ void epilogue(const f32x16 (&acc)[TM][TN], int mrow, int ncol, int lane, int z) const {

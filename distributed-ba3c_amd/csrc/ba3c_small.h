@@ -22,7 +22,7 @@ static_assert(UPD_CHUNK % 256 == 0, "whole elements per thread");
 // terms[n] = {log(p_a+1e-6)*adv, sum p log(p+1e-6), (V-R)^2, adv, V, max p, 0, 0}
 // ---------------------------------------------------------------------------------------
 struct HeadsArgs {
-  const float* h;
+  float* h;
   const float* piW;
   const float* pib;
   const float* vW;
@@ -37,6 +37,16 @@ struct HeadsArgs {
   float* terms;
   int B, F, A, train, legacy;
   float beta, explore, invB;
+  // fc1's split-K finish, fused: h = sum_z fcpart[z] in z order (+ bias, ReLU, positive count
+  // for the legacy FC), written to `h` for the backward pass.  The split is fixed (FC_SPLIT
+  // chunks of FC_KCHUNK), so every row's summation order — its rounding — is the same at any batch
+  const float* fcpart;       // [fc_split][B][F]; null: h is already final
+  int fc_split, per, wstride;
+  const float* fc_w1;        // fc1 split 0 base (legacy bias rows)
+  unsigned long long* relu_count;
+  // training: the last workgroup to finish reduces terms into the TfDictOp scalars
+  unsigned long long* done;  // completion counter (zero on entry; reset by the last workgroup)
+  double* scalars;           // null: no scalars
 };
 
 // The per-sample head arithmetic runs in fp64: the softmax gradient
@@ -52,18 +62,31 @@ __device__ __forceinline__ double wave_max_d(double v) {
 // One wave per sample; after the dot products lane a < A owns action a, so the softmax /
 // log / gradient run once per lane (one exp and one log per lane instead of MAXA of each,
 // masked, in every lane) with wave reductions for the sums and maxima.
-__global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
-  const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n >= p.B) return;
+__device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane) {
   const int A = p.A;
   double acc[MAXA];
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) acc[a] = 0.0;
   double accv = 0.0;
-  const float* hn = p.h + (size_t)n * p.F;
+  float* hn = p.h + (size_t)n * p.F;
+  unsigned long long pos = 0;
+  const size_t MN = (size_t)p.B * p.F;
   for (int f = lane; f < p.F; f += 64) {
-    const double hv = hn[f];
+    float h32;
+    if (p.fcpart) {
+      const size_t e = (size_t)n * p.F + f;
+      h32 = p.fcpart[e];
+      for (int z = 1; z < p.fc_split; ++z) h32 += p.fcpart[(size_t)z * MN + e];
+      if (p.legacy) {
+        const int sidx = f / p.per;
+        h32 = fmaxf(h32 + p.fc_w1[sidx * p.wstride + 1600 * p.per + (f - sidx * p.per)], 0.f);
+        pos += h32 > 0.f;
+      }
+      hn[f] = h32;
+    } else {
+      h32 = hn[f];
+    }
+    const double hv = h32;
     const float* wr = p.piW + (size_t)f * A;
 #pragma unroll
     for (int a = 0; a < MAXA; ++a)
@@ -79,6 +102,7 @@ __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
       if (lane == a) z = za;
     }
   }
+  if (p.fcpart && p.legacy && p.relu_count) relu_count_add(p.relu_count, pos, lane);
   const double V = wave_sum_d(accv) + (double)p.vb[0];
   // softmax(z)  (tf.nn.softmax: exp(z - max) / sum)
   const double zmax = wave_max_d(mine ? z : -INFINITY);
@@ -138,10 +162,9 @@ __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   }
 }
 
-// Deterministic reduction of the per-sample terms into the TfDictOp scalars.
-__global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B, float beta,
-                                                      const unsigned long long* relu_count,
-                                                      double* out) {
+// Deterministic reduction of the per-sample terms into the TfDictOp scalars (one workgroup).
+__device__ __forceinline__ void scalars_block(const float* terms, int B, float beta,
+                                              const unsigned long long* relu_count, double* out) {
   __shared__ double red[6][256];
   const int t = threadIdx.x;
   double s[6] = {0, 0, 0, 0, 0, 0};
@@ -188,6 +211,33 @@ __global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B,
     out[5] = red[4][0] / Bd;
     out[6] = red[5][0];
     out[7] = (double)relu_total;
+  }
+}
+
+__global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B, float beta,
+                                                      const unsigned long long* relu_count,
+                                                      double* out) {
+  scalars_block(terms, B, beta, relu_count, out);
+}
+
+// One wave per sample (heads_sample); in training with `scalars`, the last workgroup to
+// finish (completion counter, release/acquire fences) runs the scalar reduction, so the step
+// needs no separate scalars launch.  No early return: every wave reaches the barriers.
+__global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n < p.B) heads_sample(p, n, lane);
+  if (p.train && p.scalars) {                 // uniform over the grid
+    __shared__ int last;
+    __threadfence();                          // release this workgroup's terms / ReLU counts
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(p.done, 1ull) == (unsigned long long)(gridDim.x - 1);
+    __syncthreads();
+    if (last) {
+      __threadfence();                        // acquire every other workgroup's writes
+      scalars_block(p.terms, p.B, p.beta, p.relu_count, p.scalars);
+      if (threadIdx.x == 0) *p.done = 0ull;
+    }
   }
 }
 

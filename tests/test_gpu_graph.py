@@ -55,19 +55,27 @@ def test_captured_step_replays_match_eager_steps():
         np.testing.assert_array_equal(s_cap.cpu().numpy(), s_eag.cpu().numpy())
 
 
-def test_side_stream_weight_gradients_match_single_stream(monkeypatch):
-    """BA3C_OVERLAP=1 runs the backward weight-gradient kernels on a second HIP stream
-    (fork/join events, own split-K partials for conv0): eager and graph-captured steps must
-    equal the single-stream ones bit for bit."""
+@pytest.mark.parametrize("mode", ["1", "auto"])
+def test_side_stream_weight_gradients_match_single_stream(monkeypatch, mode):
+    """BA3C_OVERLAP=1 (and the default for batches <= 128) runs the backward weight-gradient
+    kernels on a second HIP stream (fork/join events, own split-K partials for conv0): eager
+    and graph-captured steps must equal the single-stream (BA3C_OVERLAP=0) ones bit for bit,
+    TfDictOp scalars included."""
     B = 64
     bs = _batches(B, 4)
+    monkeypatch.setenv("BA3C_OVERLAP", "0")
     ref = _trainer(B)
     for b in bs[1:]:
         ref.train_step(*b)
-    monkeypatch.setenv("BA3C_OVERLAP", "1")
+    ref_scalars = ref.model.scalars_dict()
+    if mode == "auto":
+        monkeypatch.delenv("BA3C_OVERLAP")
+    else:
+        monkeypatch.setenv("BA3C_OVERLAP", mode)
     eager = _trainer(B)
     for b in bs[1:]:
         eager.train_step(*b)
+    assert eager.model.scalars_dict() == ref_scalars
     cap = _trainer(B)
     static = tuple(t.clone() for t in bs[0])
     replay = cap.capture_step(*static, warmup=2)
