@@ -4,7 +4,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libba3c.so")
+# BA3C_LIB: an alternative in-tree build of the same ABI (A/B experiments, scripts/gpu_abl.sh)
+LIB_PATH = os.environ.get("BA3C_LIB") or os.path.join(_HERE, "libba3c.so")
 
 BA3C_OK = 0
 OPT_IDS = {"adam": 0, "gd": 1, "adagrad": 2, "adadelta": 3, "momentum": 4, "rms": 5}

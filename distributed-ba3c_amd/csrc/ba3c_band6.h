@@ -22,6 +22,10 @@
 #pragma once
 #include "ba3c_split.h"
 
+#ifndef BA3C_STAGE_NPT
+#define BA3C_STAGE_NPT 16   // staging loads in flight per thread (one-band kernels)
+#endif
+
 namespace ba3c {
 
 // G: BandGeom (ba3c_conv.h).  PP_: pixel pitch in bytes (>= 6 KPH), RPX_: extra row bytes,
@@ -305,13 +309,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
   const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
   unsigned long long pos = 0;
   float omax = 0.f;
+  // every staging load of the band in flight at once (one global round trip, not two)
   if constexpr (L::NPH == 1) {
-    O::stage(a, lds, tid, img, y0, rows_out, 0, asc);
+    O::template stage<BA3C_STAGE_NPT>(a, lds, tid, img, y0, rows_out, 0, asc);
     __syncthreads();
   }
   O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [&](int ph) {
     if (ph) __syncthreads();                                // previous phase's reads are done
-    O::stage(a, lds, tid, img, y0, rows_out, ph, asc);
+    O::template stage<BA3C_STAGE_NPT>(a, lds, tid, img, y0, rows_out, ph, asc);
     __syncthreads();
   });
   if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);

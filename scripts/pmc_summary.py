@@ -28,8 +28,9 @@ SHORT = [  # (regex on the kernel symbol, bench kernel id)
     (r"FcFwd", "fc1_fwd"), (r"FcDgrad", "fc1_dgrad"),
     (r"gemm6?_kernel<128, 64, 2, 2, ba3c::BatchWgrad", "fc1_wgrad"),
     (r"gemm6?_kernel<128, 32, 4, 1, ba3c::BatchWgrad", "head_wgrad"),
-    (r"heads_kernel", "heads"), (r"wgrad_reduce_kernel", "wgrad_reduce"),
+    (r"heads_kernel", "heads"), (r"wgrad_reduce(_all)?_kernel", "wgrad_reduce"),
     (r"update_kernel", "update"), (r"sumsq_kernel", "sumsq"),
+    (r"wprep6?_kernel", "wprep"), (r"scalars_kernel", "scalars"),
 ]
 
 

@@ -150,3 +150,79 @@ def test_simulator_processes_and_master_protocol():
     # every simulator contributed datapoints, episodes ended and n-step parses happened
     assert len({e[1] for e in master.log if e[0] == "msg"}) == n
     assert any(dp[5] for dp in master.queue) and any(not dp[5] for dp in master.queue)
+
+
+def test_batched_master_rounds_match_per_message_memory_logic():
+    """BatchedSimulatorMaster (one batch_policy call per round) over real simulator processes:
+    its datapoints equal the oracle's restatement of the per-message master replayed on the
+    same message log and decisions, and the actions are np.random.choice draws of one
+    RandomState in arrival order."""
+    from ba3c_amd.simulator_gpu import BatchedSimulatorMaster
+
+    d = tempfile.mkdtemp(prefix="ba3c_ipcb_")
+    c2s, s2c = "ipc://" + os.path.join(d, "c2s"), "ipc://" + os.path.join(d, "s2c")
+    n = 4
+    rs = np.random.RandomState(21)
+    log = []
+
+    def batch_policy(states):
+        probs = np.array([[0.1, 0.2, 0.3, 0.4] if int(s.sum()) % 2 else [0.25] * 4 for s in states])
+        values = np.array([float(s[:, :, -1].mean()) / 255.0 for s in states])
+        actions = np.array([rs.choice(4, p=p) for p in probs])
+        log.append(("round", [int(s.sum()) for s in states], actions.tolist(), values.tolist()))
+        return probs, values, actions
+
+    class Master(BatchedSimulatorMaster):
+        def handle(self, msg):
+            ident, state, reward, is_over, ts, alive = msg
+            if alive and not self._stop_req.is_set():
+                log.append(("msg", ident, float(reward), bool(is_over)))
+            return super(Master, self).handle(msg)
+
+        def _on_state(self, state, ident):
+            log.append(("pending", ident[0]))
+            super(Master, self)._on_state(state, ident)
+
+    master = Master(c2s, s2c, n, batch_policy=batch_policy, max_wait=0.01)
+    procs = S.start_simulators(S.SyntheticSimulatorWorker, n, c2s, s2c, seed=200)
+    master.start()
+    t0 = time.time()
+    while len(master.queue) < 300 and time.time() - t0 < 60:
+        time.sleep(0.02)
+    master.stop()
+    master.join(timeout=30)
+    for p in procs:
+        p.join(timeout=30)
+    master.close()
+    assert not master.is_alive() and master.is_done
+    assert all(p.exitcode == 0 for p in procs)
+    assert len(master.queue) >= 300
+    assert max(master.round_sizes) > 1 and max(master.round_sizes) <= n   # real batching
+
+    # replay: messages update memories in arrival order; a round's decisions are applied in
+    # the order its states were queued (== the mirror's on_state order)
+    mirror = O.SimulatorMasterMirror()
+    pend = []
+    for e in log:
+        if e[0] == "msg":
+            mirror.on_message(e[1], e[2], e[3])
+        elif e[0] == "pending":
+            pend.append(e[1])
+        else:
+            _, sums, acts, vals = e
+            assert len(sums) == len(pend)
+            for ident, ssum, a, v in zip(pend, sums, acts, vals):
+                mirror.on_state(ident, ssum, a, v)
+            pend = []
+    got = master.queue[:len(mirror.queue)]
+    assert len(mirror.queue) == len(master.queue)
+    for (st, act, R, ts, init_r, over), (tr, R_ref, init_ref, over_ref) in zip(got, mirror.queue):
+        assert int(st.sum()) == tr["state"] and act == tr["action"]
+        assert R == R_ref and float(init_r) == float(init_ref) and over == over_ref
+    # the decisions are one RandomState stream consumed in arrival order
+    rs2 = np.random.RandomState(21)
+    for e in log:
+        if e[0] == "round":
+            for ssum, a in zip(e[1], e[2]):
+                p = [0.1, 0.2, 0.3, 0.4] if ssum % 2 else [0.25] * 4
+                assert rs2.choice(4, p=p) == a
