@@ -295,15 +295,14 @@ struct Band6Ops {
 };
 
 // One workgroup = one band (image x RB output rows); two workgroups per CU overlap one's
-// staging with the other's MFMAs.
+// staging with the other's MFMAs.  The body takes its band index and LDS from the caller, so
+// a multi-job launch (ba3c_multi.h) can run it beside another kernel's workgroups.
 template <class L>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6_kernel(const Band6Args a) {
+__device__ __forceinline__ void band6_body(const Band6Args& a, int bx, char* lds) {
   using O = Band6Ops<L>;
-  __shared__ uint4 lds4[L::LDS_BYTES / 16];
-  char* lds = reinterpret_cast<char*>(lds4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int img, y0, rows_out;
-  O::band_geom(blockIdx.x, img, y0, rows_out);
+  O::band_geom(bx, img, y0, rows_out);
   const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
   const float asc = exp2i(ka), us1 = exp2i(-ka);
   const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
@@ -321,6 +320,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
   });
   if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
   if (L::G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
+}
+
+template <class L>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6_kernel(const Band6Args a) {
+  __shared__ uint4 lds4[L::LDS_BYTES / 16];
+  band6_body<L>(a, blockIdx.x, reinterpret_cast<char*>(lds4));
 }
 
 // Pipelined persistent variant (NPH == 1 layouts): one 512-thread workgroup per CU walks

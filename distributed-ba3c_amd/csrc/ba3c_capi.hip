@@ -18,6 +18,7 @@
 #include "ba3c_band6.h"
 #include "ba3c_conv.h"
 #include "ba3c_gemm6.h"
+#include "ba3c_multi.h"
 #include "ba3c_problems.h"
 #include "ba3c_rollout.h"
 #include "ba3c_small.h"
@@ -93,6 +94,16 @@ struct ba3c_handle {
   // backward kernel is a few latency-bound workgroups, so the weight-gradient chain runs in
   // the input-gradient chain's shadow.
   int overlap = 2;
+  // batches <= OVERLAP_B on the split path: each layer's input- and weight-gradient kernels
+  // run as ONE multi-job launch (ba3c_multi.h) on the main stream instead of on two streams
+  // joined by events (r02k trace at B=32: 6-11 us of idle queue per fork / join).
+  // BA3C_MULTI=0: side stream as before.
+  bool multi = true;
+  // fused-clip optimizer applies as one clip_update_kernel launch (ba3c_small.h) when the chunk
+  // count fits one workgroup per CU; its grid-barrier words live in `bar` (device, zeroed at
+  // create).  BA3C_FUSED_UPDATE=0: sumsq_kernel + update_kernel.
+  bool fused_update = true;
+  GridBarrier* bar = nullptr;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -163,6 +174,10 @@ using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
 using GWg2 = WgGeom<18, 18, 32, 5, 5, 64, 7, false, 2>;
 constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
 constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workgroups
+// conv1 weight-gradient workgroups: ~4 bands each, at least 64 (at B=32 one band per
+// workgroup made 256 partial slabs of 100 KB — 26 MB written and read back by the reduction
+// for 3.3 MB of input).  A function of B alone, so every launch path sums the same slabs.
+inline int conv1_wgrad_p(int B) { return std::max(64, std::min(W6_P1, B * 9 / 4)); }
 constexpr int FW_P0S = 512;   // conv0s_fwd_kernel: persistent, two workgroups per CU
 constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
@@ -371,13 +386,41 @@ struct SplitIO {
   int amax_in, wjob, amax_out;
 };
 
+template <class L>
+Band6Args band6_args(ba3c_handle* h, const BandArgs& a, const Workspace& w, int wt_off, SplitIO io) {
+  return Band6Args{a.src, a.code, w.wt6 + L::NS * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch,
+                   w.am(io.amax_in, h), w.wexp + io.wjob, io.amax_out >= 0 ? w.am(io.amax_out, h) : nullptr};
+}
+
+// One launch of up to three independent jobs (ba3c_multi.h); W2: the two-workgroups-per-CU
+// register budget of the band / weight-gradient kernels.
+template <bool W2, class J0, class J1, class J2 = NoJob>
+int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const typename J1::Args& a1, dim3 g1,
+                 const typename J2::Args& a2 = typename J2::Args{}, dim3 g2 = dim3(0, 1, 1)) {
+  MultiGrid g;
+  const dim3 gs[3] = {g0, g1, g2};
+  int end = 0;
+  for (int j = 0; j < 3; ++j) {
+    g.gx[j] = (int)gs[j].x;
+    g.gy[j] = (int)gs[j].y;
+    end += (int)(gs[j].x * gs[j].y * gs[j].z);
+    g.end[j] = end;
+  }
+  if (end == 0) return BA3C_OK;
+  if constexpr (W2)
+    hipLaunchKernelGGL((multi_kernel_w2<J0, J1, J2>), dim3(end), dim3(256), 0, s, a0, a1, a2, g);
+  else
+    hipLaunchKernelGGL((multi_kernel<J0, J1, J2>), dim3(end), dim3(256), 0, s, a0, a1, a2, g);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
 // LP: the layout of the pipelined persistent variant (conv_band6p_kernel), used when the
 // launch has >= 4 bands per CU
 template <class L, class LP = L>
 int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
                  int wt_off, SplitIO io, bool pipelined = false) {
-  const Band6Args b{a.src, a.code, w.wt6 + L::NS * (size_t)wt_off, a.out, a.out_code, a.relu_count, a.batch,
-                    w.am(io.amax_in, h), w.wexp + io.wjob, io.amax_out >= 0 ? w.am(io.amax_out, h) : nullptr};
+  const Band6Args b = band6_args<L>(h, a, w, wt_off, io);
   const int nbands = a.batch * L::G::NBANDS;
   {
     ProbeScope ps(h, s, kid);
@@ -425,13 +468,23 @@ int launch_wgband(ba3c_handle* h, hipStream_t s, int kid, const WgArgs& a, int p
 
 // split weight-gradient kernel + deterministic reduction into the flat HWIO grads
 template <class G>
+dim3 wgrad6_grid(int pmax, int batch) {
+  return dim3(std::min(pmax, batch * G::NBANDS), G::NCG * G::NOG);
+}
+template <class G>
+int reduce_wgrad6(ba3c_handle* h, hipStream_t s, const Wg6Args& a, int P, float* dst);
+template <class G>
 int launch_wgrad6(ba3c_handle* h, hipStream_t s, int kid, const Wg6Args& a, int pmax, float* dst) {
-  const int P = std::min(pmax, a.batch * G::NBANDS);
+  const dim3 grid = wgrad6_grid<G>(pmax, a.batch);
   {
     ProbeScope ps(h, s, kid);
-    hipLaunchKernelGGL(wgrad6_kernel<G>, dim3(P, G::NCG * G::NOG), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(wgrad6_kernel<G>, grid, dim3(256), 0, s, a);
   }
   HIP_TRY(hipGetLastError());
+  return reduce_wgrad6<G>(h, s, a, (int)grid.x, dst);
+}
+template <class G>
+int reduce_wgrad6(ba3c_handle* h, hipStream_t s, const Wg6Args& a, int P, float* dst) {
   ReduceMap mp{};
   mp.kind = 0;
   mp.M = G::M;
@@ -629,8 +682,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ++nfork;
     return BA3C_OK;
   };
-  // the side stream joins a graph capture of `s` through the fork events
-  if (h->side && (h->overlap == 1 || B <= OVERLAP_B)) ws = h->side;
+  // small batches on the split path: each layer's input- and weight-gradient kernels as one
+  // multi-job launch on `s` (no side stream, no events); otherwise the side stream joins a
+  // graph capture of `s` through the fork events
+  const bool mj = h->multi && h->overlap != 1 && B <= OVERLAP_B && h->band && h->b6 && h->w6 && h->g6 &&
+                  h->split && CH == 4;
+  static_assert(OVERLAP_B <= SMALL_B, "multi-job conv2 input gradient is the small-batch geometry");
+  if (!mj && h->side && (h->overlap == 1 || B <= OVERLAP_B)) ws = h->side;
   // every weight-gradient reduction is deferred into one launch at the end (RAII: an early
   // error return leaves the handle in immediate mode)
   struct DeferGuard {
@@ -648,7 +706,16 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   {
     WgradPlan pl = plan_wgrad(F + 1, A + 1, B, 128, 32);
     BatchWgrad g{w.h, w.dzv, w.part_h, F, MAXA, 1, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_HEAD_WGRAD, g, pl.S)));
+    WgradPlan plf = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
+    BatchWgrad gf{w.a3, w.dh, w.part_f, 1600, F, legacy ? 1 : 0, plf.M, plf.N, plf.K, plf.kchunk};
+    FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
+    if (mj)   // fc1 input gradient + head and fc1 weight gradients: one launch
+      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, 4>, Gemm6Job<128, 32, 4, 1, BatchWgrad, 4>,
+                          Gemm6Job<128, 64, 2, 2, BatchWgrad, 4>>(
+          s, d, dim3((d.M + 63) / 64, (d.N + 63) / 64, 1), g, dim3((pl.M + 127) / 128, (pl.N + 31) / 32, pl.S), gf,
+          dim3((plf.M + 127) / 128, (plf.N + 63) / 64, plf.S))));
+    else
+      CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_HEAD_WGRAD, g, pl.S)));
     ReduceMap mp{};
     mp.kind = 2;
     mp.M = pl.M;
@@ -664,7 +731,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   {
     WgradPlan pl = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
     BatchWgrad g{w.a3, w.dh, w.part_f, 1600, F, legacy ? 1 : 0, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 64, 2, 2>(h, ws, BA3C_K_FC1_WGRAD, g, pl.S)));
+    if (!mj) CHECK((launch_gemm<128, 64, 2, 2>(h, ws, BA3C_K_FC1_WGRAD, g, pl.S)));
     ReduceMap mp{};
     mp.kind = 1;
     mp.M = pl.M;
@@ -677,7 +744,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // fc1 input gradient -> dY3 (ReluGrad of conv3 fused)
   {
     FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
-    CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
+    if (!mj) CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
     CHECK(fork());
   }
   auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad, const float* part) {
@@ -694,15 +761,28 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   {
     WgradPlan pl = plan_wgrad(576, 64, B * 25, 128, 64);
     ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
-    CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
-    CHECK(conv_reduce(pl, 3, 64, 64, w.part_3));
     ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0,
                                            NS == 2 ? w.am(AM_DP2, h) : nullptr};
-    CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
+    if (mj) {
+      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, decltype(d), 4>, Gemm6Job<128, 64, 4, 1, decltype(g), 4>>(
+          s, d, dim3((d.M + 63) / 64, (d.N + 63) / 64, 1), g, dim3((pl.M + 127) / 128, (pl.N + 63) / 64, pl.S))));
+    } else {
+      CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
+      CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
+    }
+    CHECK(conv_reduce(pl, 3, 64, 64, w.part_3));
     CHECK(fork());
   }
   // conv2
-  {
+  if (mj) {
+    const Wg6Args wa{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)};
+    const dim3 wg = wgrad6_grid<typename LY::W2>(W6_P2, B);
+    const Band6Args da = band6_args<typename LY::C2DS>(h, BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B},
+                                                      w, WT_C2D, SplitIO{AM_DP2, 3, AM_DP1});
+    CHECK((launch_multi<true, Band6Job<typename LY::C2DS>, Wg6Job<typename LY::W2>>(
+        s, da, dim3(B * LY::C2DS::G::NBANDS), wa, wg)));
+    CHECK(reduce_wgrad6<typename LY::W2>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[2]].offset));
+  } else {
     if (h->band && h->w6) {
       CHECK(launch_wgrad6<typename LY::W2>(h, ws, BA3C_K_CONV2_WGRAD,
                                           Wg6Args{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)},
@@ -730,11 +810,19 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     CHECK(fork());
   }
   // conv1
-  {
+  if (mj) {
+    const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
+    const dim3 wg = wgrad6_grid<typename LY::W1>(conv1_wgrad_p(B), B);
+    const Band6Args da = band6_args<typename LY::C1D>(h, BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B},
+                                                     w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0});
+    CHECK((launch_multi<true, Band6Job<typename LY::C1D>, Wg6Job<typename LY::W1>>(
+        s, da, dim3(B * LY::C1D::G::NBANDS), wa, wg)));
+    CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[1]].offset));
+  } else {
     if (h->band && h->w6) {
       CHECK(launch_wgrad6<typename LY::W1>(h, ws, BA3C_K_CONV1_WGRAD,
                                           Wg6Args{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)},
-                                          W6_P1, grads + h->tensors[h->idx_conv[1]].offset));
+                                          conv1_wgrad_p(B), grads + h->tensors[h->idx_conv[1]].offset));
     } else if (h->band) {
       CHECK(launch_wgband<GWg1>(h, ws, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part_1, B}, WG_P1,
                                 grads + h->tensors[h->idx_conv[1]].offset, 32));
@@ -879,12 +967,23 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
+  if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
+  if (const char* e = getenv("BA3C_FUSED_UPDATE")) h->fused_update = !(e[0] == '0');
   if (const char* e = getenv("BA3C_PIPE")) h->pipe = (e[0] == '1');
   {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
       h->cus = n;
+  }
+  // grid-barrier words of clip_update_kernel (no device: stays null, two-launch apply)
+  if (hipMalloc(reinterpret_cast<void**>(&h->bar), sizeof(GridBarrier)) != hipSuccess) {
+    h->bar = nullptr;
+    (void)hipGetLastError();
+  } else if (hipMemset(h->bar, 0, sizeof(GridBarrier)) != hipSuccess) {
+    (void)hipFree(h->bar);
+    h->bar = nullptr;
+    (void)hipGetLastError();
   }
   if (const char* e = getenv("BA3C_C0LAY")) h->c0lay = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("BA3C_GEMM6")) h->g6 = !(e[0] == '0');
@@ -962,6 +1061,7 @@ void ba3c_destroy(ba3c_handle* h) {
     if (e) (void)hipEventDestroy(e);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->side) (void)hipStreamDestroy(h->side);
+  if (h->bar) (void)hipFree(h->bar);
   delete h;
 }
 
@@ -1100,7 +1200,27 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
   a.momentum = hp->momentum;
   a.rho = hp->rho;
   a.one_minus_rho = 1.0f - hp->rho;
+  a.beta1 = hp->beta1;
+  a.beta2 = hp->beta2;
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
+  if (fuse_clip && h->fused_update && h->bar && h->table.nchunks <= h->cus) {
+    a.clip_part = part;
+    const dim3 grid(h->table.nchunks);
+    {
+      ProbeScope ps(h, s, BA3C_K_UPDATE);
+      switch (opt) {
+        case BA3C_OPT_ADAM: hipLaunchKernelGGL(clip_update_kernel<0>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
+        case BA3C_OPT_GD: hipLaunchKernelGGL(clip_update_kernel<1>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
+        case BA3C_OPT_ADAGRAD: hipLaunchKernelGGL(clip_update_kernel<2>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
+        case BA3C_OPT_ADADELTA: hipLaunchKernelGGL(clip_update_kernel<3>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
+        case BA3C_OPT_MOMENTUM: hipLaunchKernelGGL(clip_update_kernel<4>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
+        case BA3C_OPT_RMS: hipLaunchKernelGGL(clip_update_kernel<5>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
+        default: return fail(BA3C_ERR_INVALID, "unknown optimizer id");
+      }
+    }
+    HIP_TRY(hipGetLastError());
+    return BA3C_OK;   // the Adam device powers advanced inside the launch
+  }
   if (fuse_clip) {
     hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part);
     HIP_TRY(hipGetLastError());

@@ -37,8 +37,18 @@ constexpr int tr_pitch(int rows) { return rows * 2 + (64 - (rows * 2) % 128 + 12
 // G6_DEPTH: k-tiles in flight per thread (register ring); 2 = classic one-ahead prefetch.
 // Small-batch launches (a few workgroups walking a long K each) take 4, large ones 2 (the
 // deeper ring's registers cost occupancy that the big launches need more).
+template <int BM, int BN, class P>
+struct Gemm6Lds {
+  static constexpr int TPA = tr_pitch(BM), TPB = tr_pitch(BN);
+  static constexpr int PA = P::A_KCONTIG ? BM * G6_RP : GEMM_BK * TPA;
+  static constexpr int PB = P::B_KCONTIG ? BN * G6_RP : GEMM_BK * TPB;
+  static constexpr int BYTES = 3 * (PA + PB);
+};
+
+// (bx, by, bz): the output tile and K chunk (blockIdx of a plain launch; ba3c_multi.h passes
+// its own); lds: Gemm6Lds<BM, BN, P>::BYTES, 16-byte aligned.
 template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2>
-__global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
+__device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, char* lds) {
   static_assert(WGM * WGN == 4, "4 waves per workgroup");
   constexpr int BK = GEMM_BK;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -50,11 +60,8 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
   constexpr int QA = BM / 4, QB = BN / 4;
   constexpr int RA = GEMM_THREADS / QA, RB = GEMM_THREADS / QB;
   // plane bytes and pitches of the two operands (see the layout note above)
-  constexpr int TPA = tr_pitch(BM), TPB = tr_pitch(BN);
-  constexpr int PA = P::A_KCONTIG ? BM * G6_RP : BK * TPA;
-  constexpr int PB = P::B_KCONTIG ? BN * G6_RP : BK * TPB;
-
-  __shared__ __attribute__((aligned(16))) char lds[3 * (PA + PB)];
+  constexpr int TPA = Gemm6Lds<BM, BN, P>::TPA, TPB = Gemm6Lds<BM, BN, P>::TPB;
+  constexpr int PA = Gemm6Lds<BM, BN, P>::PA, PB = Gemm6Lds<BM, BN, P>::PB;
   char* As = lds;
   char* Bs = lds + 3 * PA;
 
@@ -62,11 +69,11 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  const int m0 = bx * BM;
+  const int n0 = by * BN;
   int kbeg = 0, kend = p.K;
   if (p.kchunk > 0) {
-    kbeg = blockIdx.z * p.kchunk;
+    kbeg = bz * p.kchunk;
     kend = min(p.K, kbeg + p.kchunk);
   }
 
@@ -223,7 +230,13 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
     }
   }
 
-  p.template epilogue<TM, TN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, blockIdx.z);
+  p.template epilogue<TM, TN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, bz);
+}
+
+template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2>
+__global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
+  __shared__ __attribute__((aligned(16))) char lds[Gemm6Lds<BM, BN, P>::BYTES];
+  gemm6_body<BM, BN, WGM, WGN, P, G6_DEPTH>(p, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
 }  // namespace ba3c

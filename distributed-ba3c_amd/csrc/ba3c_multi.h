@@ -1,0 +1,103 @@
+// ba3c_multi.h — several independent kernels in ONE launch (horizontal fusion).
+//
+// At small batches (configs[1]: B=32) every backward kernel is a few latency-bound
+// workgroups.  The input gradient of a layer and its weight gradient read the same output
+// gradient and write disjoint buffers, so they can run side by side.  A second HIP stream
+// does that too, but each fork / join is an event (a barrier packet) that r02 traces show as
+// 6-11 us of idle queue per layer.  A multi-job launch puts the jobs' workgroups in one grid
+// instead: block b < end[0] runs job 0 with its own (x, y, z) decomposition, then job 1, then
+// job 2.  No event, no second queue.  Each job's body (band6_body, wgrad6_body, gemm6_body)
+// is the one its plain kernel runs, on the same inputs and with the same per-workgroup
+// indices, so every output is bit-identical to the separate launches.
+#pragma once
+#include "ba3c_band6.h"
+#include "ba3c_gemm6.h"
+#include "ba3c_wgrad6.h"
+
+namespace ba3c {
+
+// A job: its argument struct, its LDS bytes, and run(args, x, y, z, gx, lds, red4).
+struct NoJob {
+  using Args = int;
+  static constexpr int LDS = 0;
+  __device__ static void run(const Args&, int, int, int, int, char*, uint32_t*) {}
+};
+
+template <class L>
+struct Band6Job {
+  using Args = Band6Args;
+  static constexpr int LDS = L::LDS_BYTES;
+  __device__ static void run(const Args& a, int x, int, int, int, char* lds, uint32_t*) {
+    band6_body<L>(a, x, lds);
+  }
+};
+
+template <class G>
+struct Wg6Job {
+  using Args = Wg6Args;
+  static constexpr int LDS = G::X_BYTES + G::Y_BYTES;
+  __device__ static void run(const Args& a, int x, int y, int, int gx, char* lds, uint32_t* red4) {
+    wgrad6_body<G>(a, x, y, gx, lds, red4);
+  }
+};
+
+template <int BM, int BN, int WGM, int WGN, class P, int D>
+struct Gemm6Job {
+  using Args = P;
+  static constexpr int LDS = Gemm6Lds<BM, BN, P>::BYTES;
+  __device__ static void run(const Args& p, int x, int y, int z, int, char* lds, uint32_t*) {
+    gemm6_body<BM, BN, WGM, WGN, P, D>(p, x, y, z, lds);
+  }
+};
+
+// Per job: grid (gx, gy, gz) and the exclusive end of its block range in the launch.
+struct MultiGrid {
+  int gx[3], gy[3], end[3];
+};
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <class J0, class J1, class J2>
+__device__ __forceinline__ void multi_body(const typename J0::Args& a0, const typename J1::Args& a1,
+                                           const typename J2::Args& a2, const MultiGrid& g, char* lds,
+                                           uint32_t* red4) {
+  // the job index is uniform per workgroup, so every barrier inside a body is reached by all
+  // of its waves
+  const int b = blockIdx.x;
+  if (b < g.end[0]) {
+    const int r = b, xy = g.gx[0] * g.gy[0];
+    J0::run(a0, r % g.gx[0], (r % xy) / g.gx[0], r / xy, g.gx[0], lds, red4);
+  } else if (b < g.end[1]) {
+    const int r = b - g.end[0], xy = g.gx[1] * g.gy[1];
+    J1::run(a1, r % g.gx[1], (r % xy) / g.gx[1], r / xy, g.gx[1], lds, red4);
+  } else if (b < g.end[2]) {
+    const int r = b - g.end[1], xy = g.gx[2] * g.gy[2];
+    J2::run(a2, r % g.gx[2], (r % xy) / g.gx[2], r / xy, g.gx[2], lds, red4);
+  }
+}
+
+template <class J0, class J1, class J2>
+struct MultiLds {
+  static constexpr int BYTES = cmax(cmax(J0::LDS, J1::LDS), cmax(J2::LDS, 16));
+};
+
+template <class J0, class J1, class J2>
+__global__ void __launch_bounds__(256) multi_kernel(const typename J0::Args a0, const typename J1::Args a1,
+                                                    const typename J2::Args a2, const MultiGrid g) {
+  __shared__ uint4 lds4[MultiLds<J0, J1, J2>::BYTES / 16];
+  __shared__ uint32_t red4[4];
+  multi_body<J0, J1, J2>(a0, a1, a2, g, reinterpret_cast<char*>(lds4), red4);
+}
+
+// the band / weight-gradient bodies are tuned for two workgroups per CU (their plain kernels
+// carry the same attribute)
+template <class J0, class J1, class J2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+multi_kernel_w2(const typename J0::Args a0, const typename J1::Args a1, const typename J2::Args a2,
+                const MultiGrid g) {
+  __shared__ uint4 lds4[MultiLds<J0, J1, J2>::BYTES / 16];
+  __shared__ uint32_t red4[4];
+  multi_body<J0, J1, J2>(a0, a1, a2, g, reinterpret_cast<char*>(lds4), red4);
+}
+
+}  // namespace ba3c

@@ -162,12 +162,15 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
   }
 }
 
-// Deterministic reduction of the per-sample terms into the TfDictOp scalars (one workgroup).
+// Deterministic reduction of the per-sample terms into the TfDictOp scalars (one workgroup):
+// per-thread strided sums, wave butterflies, then the 4 wave results in wave order.  (A
+// 256-step serial loop over the ReLU-count partials by one thread was ~5 us of the B=32 step.)
 __device__ __forceinline__ void scalars_block(const float* terms, int B, float beta,
                                               const unsigned long long* relu_count, double* out) {
-  __shared__ double red[6][256];
-  const int t = threadIdx.x;
-  double s[6] = {0, 0, 0, 0, 0, 0};
+  __shared__ double red[6][4];
+  __shared__ unsigned long long rsum[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double s[5] = {0, 0, 0, 0, 0};
   double mx = 0.0;
   for (int n = t; n < B; n += 256) {
     const float* tn = terms + (size_t)n * NTERMS;
@@ -178,38 +181,35 @@ __device__ __forceinline__ void scalars_block(const float* terms, int B, float b
     s[4] += tn[4];
     mx = fmax(mx, (double)tn[5]);
   }
-  for (int i = 0; i < 5; ++i) red[i][t] = s[i];
-  red[5][t] = mx;
-  __shared__ unsigned long long rsum[256];
   unsigned long long rc = 0;
   if (relu_count)
     for (int i = t; i < RELU_SLOTS; i += 256) rc += relu_count[i];
-  rsum[t] = rc;
-  __syncthreads();
-  if (t == 0) {
-    unsigned long long tot = 0;
-    for (int i = 0; i < 256; ++i) tot += rsum[i];
-    rsum[0] = tot;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) s[i] = wave_sum_d(s[i]);
+  mx = wave_max_d(mx);
+  rc = wave_sum_u64(rc);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) red[i][wv] = s[i];
+    red[5][wv] = mx;
+    rsum[wv] = rc;
   }
   __syncthreads();
-  const unsigned long long relu_total = rsum[0];
-  for (int w = 128; w >= 1; w >>= 1) {
-    if (t < w) {
-      for (int i = 0; i < 5; ++i) red[i][t] += red[i][t + w];
-      red[5][t] = fmax(red[5][t], red[5][t + w]);
-    }
-    __syncthreads();
-  }
   if (t == 0) {
+    double r[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r[i] = ((red[i][0] + red[i][1]) + red[i][2]) + red[i][3];
+    const double pmax = fmax(fmax(red[5][0], red[5][1]), fmax(red[5][2], red[5][3]));
+    const unsigned long long relu_total = rsum[0] + rsum[1] + rsum[2] + rsum[3];
     const double Bd = (double)B, b = (double)beta;
-    const double pl = red[0][0], xe = red[1][0], vl = red[2][0] * 0.5;
+    const double pl = r[0], xe = r[1], vl = r[2] * 0.5;
     out[0] = (pl + xe * b + vl) / Bd;
     out[1] = pl * 128.0 / Bd;
     out[2] = xe * 128.0 / Bd * b;
     out[3] = vl * 128.0 / Bd;
-    out[4] = red[3][0] / Bd;
-    out[5] = red[4][0] / Bd;
-    out[6] = red[5][0];
+    out[4] = r[3] / Bd;
+    out[5] = r[4] / Bd;
+    out[6] = pmax;
     out[7] = (double)relu_total;
   }
 }
@@ -436,6 +436,7 @@ struct UpdateArgs {
   float lr, one_minus_b1, one_minus_b2, eps, alpha;   // adam
   float decay_c, momentum, rho, one_minus_rho;        // rms (decay_c = 1-decay), momentum, adadelta
   const float* dev_powers;  // non-null: Adam beta1^t, beta2^t read from the device (graph-safe)
+  float beta1, beta2;       // clip_update_kernel: advances dev_powers after every block read them
 };
 
 // TF-1.2 float32 scalar arithmetic of ApplyAdam: alpha = lr*sqrt(1-b2^t)/(1-b1^t)
@@ -448,6 +449,39 @@ __global__ void adam_powers_kernel(float* powers, float beta1, float beta2) {
   if (threadIdx.x == 0) {
     powers[0] = powers[0] * beta1;
     powers[1] = powers[1] * beta2;
+  }
+}
+
+// One element of the TF-1.2 optimizer applies.  `g` (the clipped / scaled gradient) is made
+// opaque first: otherwise the compiler may contract the clip product into the update's first
+// subtraction in one kernel and not in another, and the launch paths would differ in the last
+// bit (clip_kernel + update_kernel, update_kernel with the fused clip, clip_update_kernel).
+template <int OPT>
+__device__ __forceinline__ void opt_elem(float g, float& p, float& s0, float& s1, const UpdateArgs& a,
+                                         float alpha) {
+  asm volatile("" : "+v"(g));
+  if constexpr (OPT == 0) {  // ApplyAdam
+    s0 += (g - s0) * a.one_minus_b1;
+    s1 += (g * g - s1) * a.one_minus_b2;
+    p -= (s0 * alpha) / (sqrtf(s1) + a.eps);
+  } else if constexpr (OPT == 1) {  // ApplyGradientDescent
+    p -= g * a.lr;
+  } else if constexpr (OPT == 2) {  // ApplyAdagrad
+    s0 = s0 + g * g;
+    p -= g * a.lr * rsqrtf(s0);
+  } else if constexpr (OPT == 3) {  // ApplyAdadelta
+    const float acc = s0 * a.rho + g * g * a.one_minus_rho;
+    const float upd = sqrtf(s1 + a.eps) * rsqrtf(acc + a.eps) * g;
+    p -= upd * a.lr;
+    s0 = acc;
+    s1 = s1 * a.rho + upd * upd * a.one_minus_rho;
+  } else if constexpr (OPT == 4) {  // ApplyMomentum (use_nesterov=False)
+    s0 = s0 * a.momentum + g;
+    p -= s0 * a.lr;
+  } else {  // ApplyRMSProp
+    s0 += (g * g - s0) * a.decay_c;
+    s1 = s1 * a.momentum + (g * a.lr) / sqrtf(s0 + a.eps);
+    p -= s1;
   }
 }
 
@@ -485,42 +519,129 @@ __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const T
     const int i = beg + threadIdx.x + 256 * j;
     if (i >= end) continue;
     const long long k = o + i;
-    float g = gv[j];
-    g = a.clip_part ? (g * 0.1f) * f : g * a.grad_scale;
-    float p = pv[j];
-    if constexpr (OPT == 0) {  // ApplyAdam
-      float m = s0v[j], v = s1v[j];
-      m += (g - m) * a.one_minus_b1;
-      v += (g * g - v) * a.one_minus_b2;
-      p -= (m * alpha) / (sqrtf(v) + a.eps);
-      a.s0[k] = m;
-      a.s1[k] = v;
-    } else if constexpr (OPT == 1) {  // ApplyGradientDescent
-      p -= g * a.lr;
-    } else if constexpr (OPT == 2) {  // ApplyAdagrad
-      float acc = s0v[j] + g * g;
-      p -= g * a.lr * rsqrtf(acc);
-      a.s0[k] = acc;
-    } else if constexpr (OPT == 3) {  // ApplyAdadelta
-      float acc = s0v[j] * a.rho + g * g * a.one_minus_rho;
-      float au = s1v[j];
-      const float upd = sqrtf(au + a.eps) * rsqrtf(acc + a.eps) * g;
-      p -= upd * a.lr;
-      au = au * a.rho + upd * upd * a.one_minus_rho;
-      a.s0[k] = acc;
-      a.s1[k] = au;
-    } else if constexpr (OPT == 4) {  // ApplyMomentum (use_nesterov=False)
-      float acc = s0v[j] * a.momentum + g;
-      p -= acc * a.lr;
-      a.s0[k] = acc;
-    } else {  // ApplyRMSProp
-      float ms = s0v[j], mom = s1v[j];
-      ms += (g * g - ms) * a.decay_c;
-      mom = mom * a.momentum + (g * a.lr) / sqrtf(ms + a.eps);
-      p -= mom;
-      a.s0[k] = ms;
-      a.s1[k] = mom;
+    const float g = a.clip_part ? (gv[j] * 0.1f) * f : gv[j] * a.grad_scale;
+    float p = pv[j], s0 = s0v[j], s1 = s1v[j];
+    opt_elem<OPT>(g, p, s0, s1, a, alpha);
+    if constexpr (S0) a.s0[k] = s0;
+    if constexpr (S1) a.s1[k] = s1;
+    a.p[k] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused clip_by_average_norm + optimizer apply in ONE launch (one workgroup per chunk, every
+// workgroup co-resident: gridDim.x = nchunks <= CUs).  Phase 1 loads the chunk's gradient,
+// parameters and slots and publishes its sum of squares (sumsq_kernel's order: the same
+// partials, bit for bit); a grid barrier; phase 2 is update_kernel's arithmetic with the clip
+// factor of the tensor.  The gradient is read once, the data loads overlap the barrier, and
+// the Adam beta powers on the device advance inside the barrier (no adam_powers launch).
+// ---------------------------------------------------------------------------------------
+struct GridBarrier {
+  unsigned int count;   // arrivals of the running launch (reset by the last one)
+  unsigned int gen;     // generation: bumped by the last arrival
+  unsigned int err;     // 1: a wait gave up (bounded spin; results of that launch are invalid)
+  unsigned int pad;
+};
+
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// All workgroups of the grid meet here.  Every workgroup must be resident (the caller
+// guarantees gridDim.x <= CUs); the wait is bounded so a broken guarantee cannot hang the
+// device.  Data crossing the barrier must be written with st_agent and read with ld_agent
+// (device-coherent, no L2 write-back fence: an agent-scope __threadfence in each of ~90
+// workgroups cost more than the barrier saved).  Thread 0's s_waitcnt 0 completes its
+// st_agent before its arrival is counted.  `last` runs once, in the last workgroup to
+// arrive, before the others are released.
+template <class LastFn>
+__device__ __forceinline__ void grid_barrier(GridBarrier* b, LastFn&& last) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g = __hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);
+    if (__hip_atomic_fetch_add(&b->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      last();
+      __hip_atomic_store(&b->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+      __hip_atomic_store(&b->gen, g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned spins = 0;
+      while (__hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) {
+          atomicOr(&b->err, 1u);
+          break;
+        }
+      }
     }
+  }
+  __syncthreads();
+}
+
+// clip_factor over partials published with st_agent
+__device__ __forceinline__ float clip_factor_agent(const TensorTable& tt, int t, const float* part) {
+  float ss = 0.f;
+  for (int b = tt.chunk0[t] + (int)(threadIdx.x & 63); b < tt.chunk0[t + 1]; b += 64) ss += ld_agent(part + b);
+  ss = wave_sum_f(ss);
+  return fminf(rsqrtf(ss) * (float)tt.numel[t], 10.0f);
+}
+
+template <int OPT>
+__global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, const TensorTable tt,
+                                                          float* __restrict__ part, GridBarrier* bar) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const int t = table_find(tt, b);
+  const int c = b - tt.chunk0[t];
+  const int beg = c * UPD_CHUNK;
+  const int end = min(tt.numel[t], beg + UPD_CHUNK);
+  const long long o = tt.off[t];
+  constexpr int PER = UPD_CHUNK / 256;
+  constexpr bool S0 = OPT != 1, S1 = OPT == 0 || OPT == 3 || OPT == 5;
+  float gv[PER], pv[PER], s0v[PER], s1v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = beg + threadIdx.x + 256 * j;
+    gv[j] = pv[j] = s0v[j] = s1v[j] = 0.f;
+    if (i < end) {
+      const long long k = o + i;
+      gv[j] = a.g[k];
+      pv[j] = a.p[k];
+      if constexpr (S0) s0v[j] = a.s0[k];
+      if constexpr (S1) s1v[j] = a.s1[k];
+    }
+  }
+  // phase 1: the chunk's sum of squares, in sumsq_kernel's order (i = beg + tid + 256 j)
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (beg + (int)threadIdx.x + 256 * j < end) ss = fmaf(gv[j], gv[j], ss);
+  ss = block_sum_256(ss, red);
+  if (threadIdx.x == 0) st_agent(part + b, ss);
+  float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1]) : a.alpha;
+  asm volatile("" : "+v"(alpha));    // the powers are read here, before this workgroup arrives
+  grid_barrier(bar, [&]() {
+    if (OPT == 0 && a.dev_powers) {   // every workgroup has read the powers before arriving
+      float* pw = const_cast<float*>(a.dev_powers);
+      pw[0] = pw[0] * a.beta1;
+      pw[1] = pw[1] * a.beta2;
+    }
+  });
+  // phase 2: update_kernel's arithmetic (fused clip)
+  const float f = clip_factor_agent(tt, t, part);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = beg + threadIdx.x + 256 * j;
+    if (i >= end) continue;
+    const long long k = o + i;
+    float p = pv[j], s0 = s0v[j], s1 = s1v[j];
+    opt_elem<OPT>((gv[j] * 0.1f) * f, p, s0, s1, a, alpha);
+    if constexpr (S0) a.s0[k] = s0;
+    if constexpr (S1) a.s1[k] = s1;
     a.p[k] = p;
   }
 }

@@ -66,19 +66,19 @@ struct Wg6Args {
   const uint32_t* amax_dp; // NS = 2: per-image max |dP| slots
 };
 
+// bx / by / gx: the workgroup's band start, channel group and the persistent stride (blockIdx.x,
+// blockIdx.y, gridDim.x of a plain launch; ba3c_multi.h passes its own); xs: X_BYTES + Y_BYTES
+// of LDS, red4: 4 words of LDS scratch.
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wgrad6_kernel(const Wg6Args a) {
+__device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, int gx, char* xs, uint32_t* red4) {
   using SP = SplitP<G::NS>;
-  __shared__ uint4 lds4[(G::X_BYTES + G::Y_BYTES) / 16];
-  char* xs = reinterpret_cast<char*>(lds4);
   // NS = 2: both operands scaled by their whole tensor's max (the sum runs over images)
-  __shared__ uint32_t red4[4];
   const int kx = G::NS == 2 ? amax_exp(amax_all(a.amax_x, a.batch, red4)) : 0;
   const int ky = G::NS == 2 ? amax_exp(amax_all(a.amax_dp, a.batch, red4)) : 0;
   const float xsc = exp2i(kx), ysc = exp2i(ky);
   char* ys = xs + G::X_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int cg = blockIdx.y / G::NOG, og = blockIdx.y - cg * G::NOG;
+  const int cg = by / G::NOG, og = by - cg * G::NOG;
   const int c0 = cg * G::CW, o0 = og * G::OW;
   // wave w owns a contiguous run of taps and both 16-column n-blocks, so every X fragment it
   // reads from LDS feeds two MFMA chains (LDS reads per MFMA 1.08 -> 0.64)
@@ -170,16 +170,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
     }
   };
 
-  int band = blockIdx.x;
+  int band = bx;
   if (band < nbands) load_band(band);
-  for (; band < nbands; band += gridDim.x) {
+  for (; band < nbands; band += gx) {
     const int img = band / G::NBANDS;
     const int rows_out = min(G::RB, G::HO - (band - img * G::NBANDS) * G::RB);
     const int kvalid = rows_out * G::WO;
     __syncthreads();                                      // previous band's LDS reads done
     store_band(band);
     __syncthreads();
-    if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
+    if (band + gx < nbands) load_band(band + gx);
 
 #pragma unroll 1
     for (int s = 0; s < G::KS; ++s) {
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
   }
 
   // ---- epilogue: C layout 16x16: lane holds column (lane & 15) = o, rows 4*(lane>>4)+r = c ----
-  float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
+  float* pz = a.part + (size_t)bx * G::M * G::COUT;
   const float us1 = exp2i(-kx), us2 = exp2i(-ky);
 #pragma unroll
   for (int t = 0; t < G::TW; ++t) {
@@ -242,6 +242,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
       }
     }
   }
+}
+
+template <class G>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wgrad6_kernel(const Wg6Args a) {
+  __shared__ uint4 lds4[(G::X_BYTES + G::Y_BYTES) / 16];
+  __shared__ uint32_t red4[4];
+  wgrad6_body<G>(a, blockIdx.x, blockIdx.y, gridDim.x, reinterpret_cast<char*>(lds4), red4);
 }
 
 }  // namespace ba3c

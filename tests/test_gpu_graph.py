@@ -55,23 +55,31 @@ def test_captured_step_replays_match_eager_steps():
         np.testing.assert_array_equal(s_cap.cpu().numpy(), s_eag.cpu().numpy())
 
 
-@pytest.mark.parametrize("mode", ["1", "auto"])
-def test_side_stream_weight_gradients_match_single_stream(monkeypatch, mode):
-    """BA3C_OVERLAP=1 (and the default for batches <= 128) runs the backward weight-gradient
-    kernels on a second HIP stream (fork/join events, own split-K partials for conv0): eager
-    and graph-captured steps must equal the single-stream (BA3C_OVERLAP=0) ones bit for bit,
-    TfDictOp scalars included."""
+@pytest.mark.parametrize("mode", ["side", "multi", "side_auto", "fused_update"])
+def test_backward_launch_paths_match_single_stream(monkeypatch, mode):
+    """At B <= 128 the backward runs either as multi-job launches (default: each layer's input-
+    and weight-gradient kernels in one grid, ba3c_multi.h) or with the weight gradients on a
+    second HIP stream (BA3C_MULTI=0, or BA3C_OVERLAP=1: fork/join events); the fused-clip Adam
+    apply is one grid-barrier launch (clip_update_kernel) unless BA3C_FUSED_UPDATE=0.  Eager and
+    graph-captured steps of every variant must equal the plainest path (one stream, one kernel
+    per product, sumsq + update launches) bit for bit, TfDictOp scalars included."""
     B = 64
     bs = _batches(B, 4)
-    monkeypatch.setenv("BA3C_OVERLAP", "0")
+    plain = {"BA3C_OVERLAP": "0", "BA3C_MULTI": "0", "BA3C_FUSED_UPDATE": "0"}
+    variant = {"side": {"BA3C_OVERLAP": "1"},
+               "multi": {},
+               "side_auto": {"BA3C_MULTI": "0"},
+               "fused_update": {"BA3C_OVERLAP": "0", "BA3C_MULTI": "0"}}[mode]
+    for k, v in plain.items():
+        monkeypatch.setenv(k, v)
     ref = _trainer(B)
     for b in bs[1:]:
         ref.train_step(*b)
     ref_scalars = ref.model.scalars_dict()
-    if mode == "auto":
-        monkeypatch.delenv("BA3C_OVERLAP")
-    else:
-        monkeypatch.setenv("BA3C_OVERLAP", mode)
+    for k in plain:
+        monkeypatch.delenv(k)
+    for k, v in variant.items():
+        monkeypatch.setenv(k, v)
     eager = _trainer(B)
     for b in bs[1:]:
         eager.train_step(*b)
@@ -87,3 +95,6 @@ def test_side_stream_weight_gradients_match_single_stream(monkeypatch, mode):
     want = ref.engine.params.cpu().numpy()
     np.testing.assert_array_equal(eager.engine.params.cpu().numpy(), want)
     np.testing.assert_array_equal(cap.engine.params.cpu().numpy(), want)
+    for s_cap, s_ref in zip(cap.optimizer.slots, ref.optimizer.slots):
+        np.testing.assert_array_equal(s_cap.cpu().numpy(), s_ref.cpu().numpy())
+    assert cap.optimizer.powers() == ref.optimizer.powers()
