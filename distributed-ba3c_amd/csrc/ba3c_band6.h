@@ -396,23 +396,23 @@ struct WPrep6Args {
   int c0lay;               // conv0 forward LDS layout (its K order: conv0_wtap)
 };
 
+// (bx, by, gx): blockIdx.x, blockIdx.y, gridDim.x of a plain launch; red4: 4 floats of LDS
 template <int NS>
-__global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
-  const int y = blockIdx.y;
-  __shared__ float red4[4];
+__device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by, int gx, float* red4) {
+  const int y = by;
   if (y == 0) {
     if (a.relu)
-      for (int i = blockIdx.x * 256 + threadIdx.x; i < RELU_WORDS; i += gridDim.x * 256) a.relu[i] = 0ull;
+      for (int i = bx * 256 + threadIdx.x; i < RELU_WORDS; i += gx * 256) a.relu[i] = 0ull;
     if (a.amax)
-      for (int i = blockIdx.x * 256 + threadIdx.x; i < a.n_amax; i += gridDim.x * 256) a.amax[i] = 0u;
+      for (int i = bx * 256 + threadIdx.x; i < a.n_amax; i += gx * 256) a.amax[i] = 0u;
   }
   if (y == a.jobs.njobs) {
     int k = 0;
     if constexpr (NS == 2) {
       k = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, red4)));
-      if (blockIdx.x == 0 && threadIdx.x == 0) a.wexp[4] = k;
+      if (bx == 0 && threadIdx.x == 0) a.wexp[4] = k;
     }
-    conv0s_wprep_one<NS>(a.w0, a.wb0, blockIdx.x * 256 + threadIdx.x, k, a.c0lay);
+    conv0s_wprep_one<NS>(a.w0, a.wb0, bx * 256 + threadIdx.x, k, a.c0lay);
     return;
   }
   const WPrepJob& j = a.jobs.job[y];
@@ -441,11 +441,11 @@ __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
     __syncthreads();
     const int k = amax_exp(__float_as_uint(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]))));
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.wexp[y] = k;
+    if (bx == 0 && threadIdx.x == 0) a.wexp[y] = k;
     sc = exp2i(k);
   }
   uint16_t* dst = a.wt6 + NS * (size_t)a.off[y];
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < j.n; e += gridDim.x * 256) {
+  for (int e = bx * 256 + threadIdx.x; e < j.n; e += gx * 256) {
     const float v = wprep_value(j, e);
     if constexpr (NS == 3) {
       uint32_t hi, mid, lo;
@@ -460,6 +460,12 @@ __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
       dst[j.n + e] = (uint16_t)lo;
     }
   }
+}
+
+template <int NS>
+__global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
+  __shared__ float red4[4];
+  wprep6_body<NS>(a, blockIdx.x, blockIdx.y, gridDim.x, red4);
 }
 
 }  // namespace ba3c

@@ -223,7 +223,10 @@ WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN) {
 
 // geometry constants (train.py:92, :177-212)
 constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
-constexpr int FC_KCHUNK = 416, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;   // FC1 fwd split-K
+// FC1 fwd split-K: 10 fixed chunks of 5 k-tiles (batch-independent rounding).  r02: 416 (4
+// chunks of 13 k-tiles) left B=32 with 8 workgroups walking 13 dependent k-tiles (17.6 us)
+constexpr int FC_KCHUNK = 160, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;
+static_assert(FC_SPLIT <= FC_SPLIT_MAX, "heads kernel finishes at most FC_SPLIT_MAX chunks");
 static_assert(FC_KCHUNK % GEMM_BK == 0, "k-chunk of whole k-tiles");
 
 // conv0's weight gradient runs on the main stream while the other weight gradients run on
@@ -495,6 +498,52 @@ int reduce_wgrad6(ba3c_handle* h, hipStream_t s, const Wg6Args& a, int P, float*
   return launch_reduce(h, s, a.part, P, mp);
 }
 
+// Split-path weight preparation arguments (wprep6_kernel): every job, the conv0 fragments and
+// the zeroing of the ReLU counters / max slots.
+WPrep6Args wprep6_args(ba3c_handle* h, const float* prm, const Workspace& w, bool train) {
+  const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
+  const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
+  WPrep6Args pa{};
+  WPrepArgs& a = pa.jobs;
+  a.job[0] = WPrepJob{W1, w.wt + WT_C1F, 5, 5, 32, 32, 0, 800 * 32};
+  a.job[1] = WPrepJob{W2, w.wt + WT_C2F, 5, 5, 32, 64, 0, 800 * 64};
+  a.job[2] = WPrepJob{W1, w.wt + WT_C1D, 5, 5, 32, 32, 1, 800 * 32};
+  a.job[3] = WPrepJob{W2, w.wt + WT_C2D, 5, 5, 32, 64, 1, 1600 * 32};
+  a.njobs = train ? 4 : 2;
+  pa.wt6 = w.wt6;
+  const int offs[4] = {WT_C1F, WT_C2F, WT_C1D, WT_C2D};
+  for (int j = 0; j < 4; ++j) pa.off[j] = offs[j];
+  pa.w0 = prm + h->tensors[h->idx_conv[0]].offset;
+  pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
+  pa.relu = train ? w.relu : nullptr;
+  pa.amax = w.amax;
+  pa.n_amax = AMAX_N * (1 + h->cfg.max_batch);
+  pa.wexp = w.wexp;
+  pa.c0lay = h->c0lay;
+  return pa;
+}
+
+// Small batches (split path, C == 4): the conv0 fragments + zeroing launch alone, then the
+// band-conv weight jobs run beside conv0's forward in one multi-job launch (they are only
+// needed from conv1 on).  B=32: the 8 us weight-prep launch was on the critical path.
+template <int NS>
+int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
+                            const Workspace& w, bool train) {
+  WPrep6Args first = wprep6_args(h, prm, w, train);
+  WPrep6Args rest = first;
+  first.jobs.njobs = 0;                 // job row 0 == njobs: conv0 fragments (+ zeroing)
+  rest.w0 = nullptr;                    // rows 0..njobs-1 only, no zeroing: conv0 publishes
+  rest.relu = nullptr;                  // into those counters concurrently
+  rest.amax = nullptr;
+  hipLaunchKernelGGL(wprep6_kernel<NS>, dim3(64, 1), dim3(256), 0, s, first);
+  HIP_TRY(hipGetLastError());
+  const Conv0SArgs sa{state, reinterpret_cast<const uint4*>(w.wt + WT_C0S), w.p0, train ? w.c0 : nullptr,
+                      train ? w.relu : nullptr, B, w.wexp + 4, w.am(AM_P0, h)};
+  ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
+  return launch_multi<false, Conv0SJob<NS, 2>, WPrep6Job<NS>>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)),
+                                                              rest, dim3(64, rest.jobs.njobs));
+}
+
 // [N][K] copies of the band-conv weights for this step (forward; + rotated dgrad in training)
 template <int NS>
 int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, bool train) {
@@ -509,18 +558,8 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
   const bool c0s = h->cfg.channels == 4 && h->split;
   if (h->b6) {
     // split path: one launch writes the splits (and conv0's fragments) directly
-    WPrep6Args pa{};
-    pa.jobs = a;
-    pa.wt6 = w.wt6;
-    const int offs[4] = {WT_C1F, WT_C2F, WT_C1D, WT_C2D};
-    for (int j = 0; j < 4; ++j) pa.off[j] = offs[j];
-    pa.w0 = c0s ? prm + h->tensors[h->idx_conv[0]].offset : nullptr;
-    pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
-    pa.relu = train ? w.relu : nullptr;
-    pa.amax = w.amax;
-    pa.n_amax = AMAX_N * (1 + h->cfg.max_batch);
-    pa.wexp = w.wexp;
-    pa.c0lay = h->c0lay;
+    WPrep6Args pa = wprep6_args(h, prm, w, train);
+    if (!c0s) pa.w0 = nullptr;
     hipLaunchKernelGGL(wprep6_kernel<NS>, dim3(64, a.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
     HIP_TRY(hipGetLastError());
   } else {
@@ -575,9 +614,16 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   unsigned long long* rc = train ? w.relu : nullptr;
   uint32_t* am_p0 = NS == 2 ? w.am(AM_P0, h) : nullptr;
   const SplitIO io1{AM_P0, 0, AM_P1}, io2{AM_P1, 1, -1};
-  if (h->band) CHECK(launch_wprep<NS>(h, s, prm, w, train));
+  // small batches on the split path: weight prep beside conv0's forward (one launch fewer on
+  // the critical path)
+  const bool mj = h->multi && B <= OVERLAP_B && CH == 4 && h->band && h->b6 && h->split && NS == 2 &&
+                  h->c0lay == 2;
+  if (mj) CHECK(launch_prep_conv0_multi<NS>(h, s, prm, state, B, w, train));
+  else if (h->band) CHECK(launch_wprep<NS>(h, s, prm, w, train));
   if (train) {
-    if (h->band && CH == 4) {
+    if (mj) {
+      // conv0 ran beside the weight prep above
+    } else if (h->band && CH == 4) {
       CHECK(launch_conv0_band<NS>(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
                                                  w.wt + WT_C0F, w.p0, w.c0, rc, B}, w));
     } else {
@@ -601,7 +647,9 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
       CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
     }
   } else if (h->band) {
-    if (CH == 4) {
+    if (mj) {
+      // conv0 ran beside the weight prep above
+    } else if (CH == 4) {
       CHECK(launch_conv0_band<NS>(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
                                                  w.wt + WT_C0F, w.p0, nullptr, nullptr, B}, w));
     } else {
@@ -636,7 +684,10 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   {
     ProbeScope ps(h, s, BA3C_K_FC1_FWD);
     const dim3 grid((B + 127) / 128, (F + 63) / 64, FC_SPLIT);
-    if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
+    if (h->g6 && B <= 64)   // 64-row tiles: same per-row K order, half the dead rows staged
+      hipLaunchKernelGGL((gemm6_kernel<64, 64, 2, 2, FcFwd, 4>), dim3((B + 63) / 64, grid.y, grid.z),
+                         dim3(GEMM_THREADS), 0, s, fc);
+    else if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, 4>), grid, dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);

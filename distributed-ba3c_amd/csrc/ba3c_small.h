@@ -12,6 +12,20 @@ constexpr int NTERMS = 8;       // per-sample loss terms
 constexpr int MAXT = 48;        // max tensors in the flat layout
 constexpr int UPD_CHUNK = 4096; // floats per workgroup in clip / update kernels
 static_assert(UPD_CHUNK % 256 == 0, "whole elements per thread");
+constexpr int FC_SPLIT_MAX = 16;  // fc1 split-K chunks the heads kernel can finish
+
+// Device-coherent (agent-scope) stores / loads for data that crosses workgroups inside one
+// launch.  MI355X's 8 XCDs have non-coherent L2s: a plain store + __threadfence() pays an L2
+// write-back per workgroup, these go to the coherence point directly.
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---------------------------------------------------------------------------------------
 // Heads: one wave per sample.  z = h W_pi + b_pi, V = h W_v + b_v, p = softmax(z),
@@ -75,8 +89,13 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
     float h32;
     if (p.fcpart) {
       const size_t e = (size_t)n * p.F + f;
-      h32 = p.fcpart[e];
-      for (int z = 1; z < p.fc_split; ++z) h32 += p.fcpart[(size_t)z * MN + e];
+      float pz[FC_SPLIT_MAX];                       // every chunk's load in flight, then the
+#pragma unroll                                      // sum in z order
+      for (int z = 0; z < FC_SPLIT_MAX; ++z) pz[z] = z < p.fc_split ? p.fcpart[(size_t)z * MN + e] : 0.f;
+      h32 = pz[0];
+#pragma unroll
+      for (int z = 1; z < FC_SPLIT_MAX; ++z)
+        if (z < p.fc_split) h32 += pz[z];
       if (p.legacy) {
         const int sidx = f / p.per;
         h32 = fmaxf(h32 + p.fc_w1[sidx * p.wstride + 1600 * p.per + (f - sidx * p.per)], 0.f);
@@ -158,7 +177,7 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
     t = lane == 3 ? adv : t;
     t = lane == 4 ? V : t;
     t = lane == 5 ? pmax : t;
-    p.terms[(size_t)n * NTERMS + lane] = (float)t;
+    st_agent(p.terms + (size_t)n * NTERMS + lane, (float)t);   // read by the last workgroup
   }
 }
 
@@ -174,16 +193,16 @@ __device__ __forceinline__ void scalars_block(const float* terms, int B, float b
   double mx = 0.0;
   for (int n = t; n < B; n += 256) {
     const float* tn = terms + (size_t)n * NTERMS;
-    s[0] += tn[0];
-    s[1] += tn[1];
-    s[2] += tn[2];
-    s[3] += tn[3];
-    s[4] += tn[4];
-    mx = fmax(mx, (double)tn[5]);
+    s[0] += ld_agent(tn + 0);
+    s[1] += ld_agent(tn + 1);
+    s[2] += ld_agent(tn + 2);
+    s[3] += ld_agent(tn + 3);
+    s[4] += ld_agent(tn + 4);
+    mx = fmax(mx, (double)ld_agent(tn + 5));
   }
   unsigned long long rc = 0;
   if (relu_count)
-    for (int i = t; i < RELU_SLOTS; i += 256) rc += relu_count[i];
+    for (int i = t; i < RELU_SLOTS; i += 256) rc += ld_agent(relu_count + i);
 #pragma unroll
   for (int i = 0; i < 5; ++i) s[i] = wave_sum_d(s[i]);
   mx = wave_max_d(mx);
@@ -228,13 +247,14 @@ __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n < p.B) heads_sample(p, n, lane);
   if (p.train && p.scalars) {                 // uniform over the grid
+    // terms go out with st_agent and ReLU counts with device atomics; each wave waits for its
+    // own stores before the workgroup's arrival is counted (no L2 write-back fence)
     __shared__ int last;
-    __threadfence();                          // release this workgroup's terms / ReLU counts
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) last = atomicAdd(p.done, 1ull) == (unsigned long long)(gridDim.x - 1);
     __syncthreads();
     if (last) {
-      __threadfence();                        // acquire every other workgroup's writes
       scalars_block(p.terms, p.B, p.beta, p.relu_count, p.scalars);
       if (threadIdx.x == 0) *p.done = 0ull;
     }
@@ -543,12 +563,6 @@ struct GridBarrier {
   unsigned int pad;
 };
 
-__device__ __forceinline__ void st_agent(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_agent(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // All workgroups of the grid meet here.  Every workgroup must be resident (the caller
 // guarantees gridDim.x <= CUs); the wait is bounded so a broken guarantee cannot hang the

@@ -251,12 +251,17 @@ __device__ __forceinline__ uint32_t u8pair(uint32_t a, uint32_t b) {
   else return pack_f16x2((float)a, (float)b);
 }
 
+template <int LAY>
+constexpr int conv0s_fwd_lds_bytes() { return Conv0S::SROWS * Conv0S::xp(LAY) * 8; }
+
+// bx / gx: first band and persistent stride (blockIdx.x / gridDim.x of a plain launch);
+// lds: conv0s_fwd_lds_bytes<LAY>() bytes
 template <int NS, int LAY = 2>
-__global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
+__device__ __forceinline__ void conv0s_fwd_body(const Conv0SArgs& a, int bx, int gx, char* lds) {
   using G = Conv0S;
   constexpr int XP = G::xp(LAY);
   using SP = SplitP<NS>;
-  __shared__ uint2 xs[G::SROWS * XP];               // 16-bit pixels (4 channels), 14 KB
+  uint2* xs = reinterpret_cast<uint2*>(lds);        // 16-bit pixels (4 channels), 14 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbands = a.batch * G::NBANDS;
 
@@ -292,7 +297,7 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
     }
   };
 
-  int band = blockIdx.x;
+  int band = bx;
   if (band < nbands) load_band(band);
 
   const int li = lane & 15, lq = lane >> 4;
@@ -321,12 +326,12 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
   unsigned long long pos = 0;
   // (sum_k u8 * w 2^kw) * (2^-kw / 255): scaling by a power of two commutes with the rounding
   const float oscale = NS == 2 ? (1.0f / 255.0f) * exp2i(-a.wexp[0]) : 1.0f / 255.0f;
-  for (; band < nbands; band += gridDim.x) {
+  for (; band < nbands; band += gx) {
     const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
     __syncthreads();                                 // previous band's LDS reads are done
     store_band();
     __syncthreads();
-    if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
+    if (band + gx < nbands) load_band(band + gx);
     float bmax = 0.f;
 #pragma unroll
     for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
@@ -377,6 +382,12 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
     if constexpr (NS == 2) amax_publish(a.amax_out, img, bmax, lane);
   }
   if (a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
+}
+
+template <int NS, int LAY = 2>
+__global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
+  __shared__ uint4 xs4[conv0s_fwd_lds_bytes<LAY>() / 16];
+  conv0s_fwd_body<NS, LAY>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(xs4));
 }
 
 // ---------------------------------------------------------------------------------------
