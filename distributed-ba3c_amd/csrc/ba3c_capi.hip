@@ -326,7 +326,7 @@ struct ProbeScope {
   }
 };
 
-template <int BM, int BN, int WGM, int WGN, class P>
+template <int BM, int BN, int WGM, int WGN, class P, int KS = 1>
 int launch_gemm(ba3c_handle* h, hipStream_t s, int kid, const P& p, int splits) {
   if (p.M <= 0 || p.N <= 0) return BA3C_OK;
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, splits);
@@ -334,7 +334,11 @@ int launch_gemm(ba3c_handle* h, hipStream_t s, int kid, const P& p, int splits) 
     ProbeScope ps(h, s, kid);
     // fewer workgroups than CUs: each walks its K latency-bound, so keep 4 k-tiles in flight
     const bool deep = (int)(grid.x * grid.y * grid.z) < h->cus;
-    if (h->g6 && deep)
+    if (KS == 2 && h->g6 && deep)
+      hipLaunchKernelGGL((gemm6_kernel<BM, BN, WGM, WGN, P, 4, KS>), grid, dim3(GEMM_THREADS * KS), 0, s, p);
+    else if (KS == 2 && h->g6)
+      hipLaunchKernelGGL((gemm6_kernel<BM, BN, WGM, WGN, P, 2, KS>), grid, dim3(GEMM_THREADS * KS), 0, s, p);
+    else if (h->g6 && deep)
       hipLaunchKernelGGL((gemm6_kernel<BM, BN, WGM, WGN, P, 4>), grid, dim3(GEMM_THREADS), 0, s, p);
     else if (h->g6)
       hipLaunchKernelGGL((gemm6_kernel<BM, BN, WGM, WGN, P>), grid, dim3(GEMM_THREADS), 0, s, p);
@@ -396,8 +400,8 @@ Band6Args band6_args(ba3c_handle* h, const BandArgs& a, const Workspace& w, int 
 }
 
 // One launch of up to three independent jobs (ba3c_multi.h); W2: the two-workgroups-per-CU
-// register budget of the band / weight-gradient kernels.
-template <bool W2, class J0, class J1, class J2 = NoJob>
+// register budget of the band / weight-gradient kernels; T512: 512-thread jobs.
+template <bool W2, class J0, class J1, class J2 = NoJob, bool T512 = false>
 int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const typename J1::Args& a1, dim3 g1,
                  const typename J2::Args& a2 = typename J2::Args{}, dim3 g2 = dim3(0, 1, 1)) {
   MultiGrid g;
@@ -410,7 +414,9 @@ int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const type
     g.end[j] = end;
   }
   if (end == 0) return BA3C_OK;
-  if constexpr (W2)
+  if constexpr (T512)
+    hipLaunchKernelGGL((multi_kernel512<J0, J1, J2>), dim3(end), dim3(512), 0, s, a0, a1, a2, g);
+  else if constexpr (W2)
     hipLaunchKernelGGL((multi_kernel_w2<J0, J1, J2>), dim3(end), dim3(256), 0, s, a0, a1, a2, g);
   else
     hipLaunchKernelGGL((multi_kernel<J0, J1, J2>), dim3(end), dim3(256), 0, s, a0, a1, a2, g);
@@ -675,7 +681,9 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
     CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
   }
   ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
-  CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
+  // K = 576 in two halves of 9 k-tiles summed in the workgroup (KS = 2) at every batch, so
+  // each output's rounding is the same whatever batch it runs in
+  CHECK((launch_gemm<64, 64, 2, 2, decltype(c3), 2>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
   // split-K: K = 1600 in FC_SPLIT fixed chunks (a 128x64 tile over all of K is one
   // workgroup's 50 serial k-tiles: latency-bound at any batch); the chunk sums (+ legacy bias,
   // ReLU, count) are finished inside the heads kernel (run_heads), which reads them anyway
@@ -814,12 +822,18 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0,
                                            NS == 2 ? w.am(AM_DP2, h) : nullptr};
+    // The input gradient's K = 576 runs in two halves summed in the workgroup (KS = 2) at
+    // every batch (each image's dP2 rounds the same in any batch, like the forward); the
+    // weight gradient takes KS = 2 for B <= OVERLAP_B on every launch path (the multi-job
+    // and side-stream paths give the same bits)
     if (mj) {
-      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, decltype(d), 4>, Gemm6Job<128, 64, 4, 1, decltype(g), 4>>(
+      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, decltype(d), 4, 2>, Gemm6Job<128, 64, 4, 1, decltype(g), 4, 2>,
+                          NoJob, true>(
           s, d, dim3((d.M + 63) / 64, (d.N + 63) / 64, 1), g, dim3((pl.M + 127) / 128, (pl.N + 63) / 64, pl.S))));
     } else {
-      CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
-      CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
+      if (B <= OVERLAP_B) CHECK((launch_gemm<128, 64, 4, 1, decltype(g), 2>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
+      else CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
+      CHECK((launch_gemm<64, 64, 2, 2, decltype(d), 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
     }
     CHECK(conv_reduce(pl, 3, 64, 64, w.part_3));
     CHECK(fork());

@@ -220,22 +220,99 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-__device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// ---- wave-wide reductions on DPP + gfx950 permlane swaps (VALU-only; ds_bpermute-based
+// __shfl_xor went through the LDS unit, ~6 round trips per reduction).  Steps: quad xor 1,
+// quad xor 2, half-row mirror, row mirror (DPP), then row pairs (v_permlane16_swap) and halves
+// (v_permlane32_swap).  Every step combines a lane with a partner that combines the same two
+// operands, so all 64 lanes end with the bit-identical result.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return __builtin_amdgcn_update_dpp(0u, x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) { return __uint_as_float(dpp32<CTRL>(__float_as_uint(v))); }
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const uint32_t lo = dpp32<CTRL>((uint32_t)u), hi = dpp32<CTRL>((uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// (even-row value, odd-row value) of this lane's row pair / (low-half, high-half) values
+__device__ __forceinline__ void swap16f(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap32f(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16d(double v, double& a, double& b) {
+  const unsigned long long u = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+  b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+__device__ __forceinline__ void swap32d(double v, double& a, double& b) {
+  const unsigned long long u = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+  b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
 }
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+struct OpAdd {
+  template <class T>
+  __device__ T operator()(T a, T b) const { return a + b; }
+};
+struct OpMax {
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+  __device__ double operator()(double a, double b) const { return fmax(a, b); }
+};
+
+// reduction over the first `w` lanes (w <= 4, 8, 16 or 64 — the others must hold the
+// identity) in every lane: the narrow forms stop after the DPP steps that cover w lanes and
+// broadcast lane 0 (v_readlane)
+template <class Op>
+__device__ __forceinline__ float wave_reduce_f(float v, Op op, int w = 64) {
+  v = op(v, dppf<0xB1>(v));
+  v = op(v, dppf<0x4E>(v));
+  if (w <= 4) return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 0));
+  v = op(v, dppf<0x141>(v));
+  if (w <= 8) return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 0));
+  v = op(v, dppf<0x140>(v));
+  if (w <= 16) return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), 0));
+  float a, b;
+  swap16f(v, a, b);
+  v = op(a, b);
+  swap32f(v, a, b);
+  return op(a, b);
+}
+template <class Op>
+__device__ __forceinline__ double wave_reduce_d(double v, Op op, int w = 64) {
+  auto bcast0 = [](double x) {
+    const unsigned long long u = __double_as_longlong(x);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, 0), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), 0);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+  };
+  v = op(v, dppd<0xB1>(v));
+  v = op(v, dppd<0x4E>(v));
+  if (w <= 4) return bcast0(v);
+  v = op(v, dppd<0x141>(v));
+  if (w <= 8) return bcast0(v);
+  v = op(v, dppd<0x140>(v));
+  if (w <= 16) return bcast0(v);
+  double a, b;
+  swap16d(v, a, b);
+  v = op(a, b);
+  swap32d(v, a, b);
+  return op(a, b);
 }
 
-__device__ __forceinline__ float wave_max_f(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ float wave_sum_f(float v) { return wave_reduce_f(v, OpAdd{}); }
+__device__ __forceinline__ double wave_sum_d(double v, int w = 64) { return wave_reduce_d(v, OpAdd{}, w); }
+__device__ __forceinline__ float wave_max_f(float v) { return wave_reduce_f(v, OpMax{}); }
 
 }  // namespace ba3c

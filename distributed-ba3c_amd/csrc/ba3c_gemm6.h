@@ -46,10 +46,15 @@ struct Gemm6Lds {
 };
 
 // (bx, by, bz): the output tile and K chunk (blockIdx of a plain launch; ba3c_multi.h passes
-// its own); lds: Gemm6Lds<BM, BN, P>::BYTES, 16-byte aligned.
-template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2>
+// its own); lds: KS * Gemm6Lds<BM, BN, P>::BYTES, 16-byte aligned.
+// KS = 2: 512 threads, two groups of 4 waves split the tile's k-tiles in halves (group 0 the
+// first ceil(n/2), group 1 the rest, each with its own staging LDS and the same trip count),
+// and group 0 adds group 1's accumulators (acc0 + acc1) before the epilogue.  Small launches
+// (a few workgroups walking a long K) run their serial k-tile chain at half the length.
+template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2, int KS = 1>
 __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, char* lds) {
-  static_assert(WGM * WGN == 4, "4 waves per workgroup");
+  static_assert(WGM * WGN == 4, "4 waves per group");
+  static_assert(KS == 1 || KS == 2, "k groups");
   constexpr int BK = GEMM_BK;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -62,10 +67,11 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
   // plane bytes and pitches of the two operands (see the layout note above)
   constexpr int TPA = Gemm6Lds<BM, BN, P>::TPA, TPB = Gemm6Lds<BM, BN, P>::TPB;
   constexpr int PA = Gemm6Lds<BM, BN, P>::PA, PB = Gemm6Lds<BM, BN, P>::PB;
-  char* As = lds;
-  char* Bs = lds + 3 * PA;
+  const int grp = KS == 2 ? (int)(threadIdx.x >> 8) : 0;
+  char* As = lds + grp * 3 * (PA + PB);
+  char* Bs = As + 3 * PA;
 
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x & 255;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -75,6 +81,14 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
   if (p.kchunk > 0) {
     kbeg = bz * p.kchunk;
     kend = min(p.K, kbeg + p.kchunk);
+  }
+  // k-tiles of this group; both groups run the same trip count (a tile past the group's
+  // kend reads the zero block)
+  int ntiles = (kend - kbeg + BK - 1) / BK;
+  if constexpr (KS == 2) {
+    ntiles = (ntiles + 1) / 2;
+    kbeg += grp * ntiles * BK;
+    kend = min(kend, kbeg + ntiles * BK);
   }
 
   typename P::ARow arow[P::A_KCONTIG ? NA : 1];
@@ -205,8 +219,9 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
   // < G6_DEPTH tail tiles are already in the ring.
 #pragma unroll
   for (int st = 0; st < G6_DEPTH - 1; ++st) load(st, kbeg + st * BK);
-  int kk = kbeg;
-  for (; kk + (G6_DEPTH - 1) * BK < kend; kk += G6_DEPTH * BK) {   // >= G6_DEPTH tiles left
+  int it = 0;
+  for (; it + G6_DEPTH - 1 < ntiles; it += G6_DEPTH) {   // >= G6_DEPTH tiles left
+    const int kk = kbeg + it * BK;
 #pragma unroll
     for (int st = 0; st < G6_DEPTH; ++st) {
       // sched barriers: the split arithmetic of a later stage would otherwise be hoisted to
@@ -222,21 +237,43 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
   }
 #pragma unroll
   for (int st = 0; st < G6_DEPTH - 1; ++st) {
-    if (kk + st * BK < kend) {                 // uniform
+    if (it + st < ntiles) {                    // uniform
       store(st);
       __syncthreads();
-      tile(kk + st * BK);
+      tile(kbeg + (it + st) * BK);
       __syncthreads();
     }
   }
 
+  if constexpr (KS == 2) {
+    // group 1 hands its accumulators to group 0 through LDS (lane-major: conflict-free)
+    float* xch = reinterpret_cast<float*>(lds);
+    constexpr int NV = TM * TN * 16;
+    static_assert(NV * 256 * 4 <= 3 * (PA + PB), "exchange fits a group's staging LDS");
+    if (grp == 1) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xch[((a * TN + b) * 16 + r) * 256 + tid] = acc[a][b][r];
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = acc[a][b][r] + xch[((a * TN + b) * 16 + r) * 256 + tid];
+  }
   p.template epilogue<TM, TN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, bz);
 }
 
-template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2>
-__global__ void __launch_bounds__(GEMM_THREADS) gemm6_kernel(const P p) {
-  __shared__ __attribute__((aligned(16))) char lds[Gemm6Lds<BM, BN, P>::BYTES];
-  gemm6_body<BM, BN, WGM, WGN, P, G6_DEPTH>(p, blockIdx.x, blockIdx.y, blockIdx.z, lds);
+template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2, int KS = 1>
+__global__ void __launch_bounds__(GEMM_THREADS * KS) gemm6_kernel(const P p) {
+  __shared__ __attribute__((aligned(16))) char lds[KS * Gemm6Lds<BM, BN, P>::BYTES];
+  gemm6_body<BM, BN, WGM, WGN, P, G6_DEPTH, KS>(p, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
 }  // namespace ba3c

@@ -41,12 +41,12 @@ struct Wg6Job {
   }
 };
 
-template <int BM, int BN, int WGM, int WGN, class P, int D>
+template <int BM, int BN, int WGM, int WGN, class P, int D, int KS = 1>
 struct Gemm6Job {
   using Args = P;
-  static constexpr int LDS = Gemm6Lds<BM, BN, P>::BYTES;
+  static constexpr int LDS = KS * Gemm6Lds<BM, BN, P>::BYTES;
   __device__ static void run(const Args& p, int x, int y, int z, int, char* lds, uint32_t*) {
-    gemm6_body<BM, BN, WGM, WGN, P, D>(p, x, y, z, lds);
+    gemm6_body<BM, BN, WGM, WGN, P, D, KS>(p, x, y, z, lds);
   }
 };
 
@@ -102,6 +102,15 @@ struct MultiLds {
 template <class J0, class J1, class J2>
 __global__ void __launch_bounds__(256) multi_kernel(const typename J0::Args a0, const typename J1::Args a1,
                                                     const typename J2::Args a2, const MultiGrid g) {
+  __shared__ uint4 lds4[MultiLds<J0, J1, J2>::BYTES / 16];
+  __shared__ uint32_t red4[4];
+  multi_body<J0, J1, J2>(a0, a1, a2, g, reinterpret_cast<char*>(lds4), red4);
+}
+
+// 512-thread jobs (gemm6 bodies with KS = 2)
+template <class J0, class J1, class J2>
+__global__ void __launch_bounds__(512) multi_kernel512(const typename J0::Args a0, const typename J1::Args a1,
+                                                       const typename J2::Args a2, const MultiGrid g) {
   __shared__ uint4 lds4[MultiLds<J0, J1, J2>::BYTES / 16];
   __shared__ uint32_t red4[4];
   multi_body<J0, J1, J2>(a0, a1, a2, g, reinterpret_cast<char*>(lds4), red4);

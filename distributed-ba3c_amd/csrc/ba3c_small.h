@@ -67,11 +67,7 @@ struct HeadsArgs {
 // p_k (g_k - sum_j p_j g_j) cancels catastrophically when the policy saturates, and fp64 here
 // costs nothing measurable (F*(A+1) FMAs per sample) while keeping the fp32 stored results
 // within rounding of the exact values.
-__device__ __forceinline__ double wave_max_d(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ double wave_max_d(double v, int w = 64) { return wave_reduce_d(v, OpMax{}, w); }
 
 // One wave per sample; after the dot products lane a < A owns action a, so the softmax /
 // log / gradient run once per lane (one exp and one log per lane instead of MAXA of each,
@@ -124,15 +120,15 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
   if (p.fcpart && p.legacy && p.relu_count) relu_count_add(p.relu_count, pos, lane);
   const double V = wave_sum_d(accv) + (double)p.vb[0];
   // softmax(z)  (tf.nn.softmax: exp(z - max) / sum)
-  const double zmax = wave_max_d(mine ? z : -INFINITY);
+  const double zmax = wave_max_d(mine ? z : -INFINITY, A);
   const double e = mine ? exp(z - zmax) : 0.0;
-  const double pr = e / wave_sum_d(e);              // 0 for lane >= A
-  const double pmax = wave_max_d(pr);
+  const double pr = e / wave_sum_d(e, A);           // 0 for lane >= A
+  const double pmax = wave_max_d(pr, A);
   if (p.probsT) {
     const double zt = z * (double)p.explore;
-    const double ztmax = wave_max_d(mine ? zt : -INFINITY);
+    const double ztmax = wave_max_d(mine ? zt : -INFINITY, A);
     const double et = mine ? exp(zt - ztmax) : 0.0;
-    const double st = wave_sum_d(et);
+    const double st = wave_sum_d(et, A);
     if (mine) p.probsT[(size_t)n * A + lane] = (float)(et / st);
   }
   if (p.probs && mine) p.probs[(size_t)n * A + lane] = (float)pr;
@@ -145,10 +141,10 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
   const double beta = (double)p.beta, invB = 1.0 / (double)p.B;
   const double pe = pr + 1e-6;
   const double lp = mine ? log(pe) : 0.0;
-  const double xent = wave_sum_d(pr * lp);
+  const double xent = wave_sum_d(pr * lp, A);
   const double lpa = __shfl(lp, act, 64);
   const double gp = mine ? ((lane == act ? adv / pe : 0.0) + beta * (lp + pr / pe)) * invB : 0.0;
-  const double sgp = wave_sum_d(gp * pr);
+  const double sgp = wave_sum_d(gp * pr, A);
   const double dz = mine ? pr * (gp - sgp) : 0.0;
   const double dV = (V - Rn) * invB;
   // [dz | dV | 0...] row for the head weight-gradient product
@@ -157,7 +153,11 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
     dza[a] = 0.0;
-    if (a < A) dza[a] = __shfl(dz, a, 64);          // uniform branch: A broadcasts only
+    if (a < A) {                                     // uniform branch: A broadcasts only
+      const unsigned long long u = __double_as_longlong(dz);
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, a), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), a);
+      dza[a] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    }
   }
   float* dhn = p.dh + (size_t)n * p.F;
   for (int f = lane; f < p.F; f += 64) {
@@ -392,10 +392,16 @@ struct TensorTable {
   int chunk0[MAXT + 1];
 };
 
+// the tensor of chunk b: largest t with chunk0[t] <= b (binary search: ~6 dependent scalar
+// loads of the kernel-argument table instead of up to n)
 __device__ __forceinline__ int table_find(const TensorTable& tt, int b) {
-  int t = 0;
-  while (t + 1 < tt.n && tt.chunk0[t + 1] <= b) ++t;
-  return t;
+  int lo = 0, hi = tt.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tt.chunk0[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
 }
 
 __device__ __forceinline__ float block_sum_256(float v, float* red) {
