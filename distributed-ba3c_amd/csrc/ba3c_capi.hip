@@ -103,7 +103,8 @@ struct ba3c_handle {
   // count fits one workgroup per CU; its grid-barrier words live in `bar` (device, zeroed at
   // create).  BA3C_FUSED_UPDATE=0: sumsq_kernel + update_kernel.
   bool fused_update = true;
-  GridBarrier* bar = nullptr;
+  // clip_update_kernel's tagged partials (nchunks words) + error flag: device, zeroed at create
+  unsigned long long* utag = nullptr;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -1041,15 +1042,6 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
       h->cus = n;
   }
-  // grid-barrier words of clip_update_kernel (no device: stays null, two-launch apply)
-  if (hipMalloc(reinterpret_cast<void**>(&h->bar), sizeof(GridBarrier)) != hipSuccess) {
-    h->bar = nullptr;
-    (void)hipGetLastError();
-  } else if (hipMemset(h->bar, 0, sizeof(GridBarrier)) != hipSuccess) {
-    (void)hipFree(h->bar);
-    h->bar = nullptr;
-    (void)hipGetLastError();
-  }
   if (const char* e = getenv("BA3C_C0LAY")) h->c0lay = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("BA3C_GEMM6")) h->g6 = !(e[0] == '0');
   if (!h->band) h->g6 = false;
@@ -1114,6 +1106,16 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   }
   tt.chunk0[tt.n] = ch;
   tt.nchunks = ch;
+  // clip_update_kernel's tagged partials + error word (no device: stays null, two-launch apply)
+  const size_t ubytes = ((size_t)tt.nchunks + 1) * sizeof(unsigned long long);
+  if (hipMalloc(reinterpret_cast<void**>(&h->utag), ubytes) != hipSuccess) {
+    h->utag = nullptr;
+    (void)hipGetLastError();
+  } else if (hipMemset(h->utag, 0, ubytes) != hipSuccess) {
+    (void)hipFree(h->utag);
+    h->utag = nullptr;
+    (void)hipGetLastError();
+  }
   *out = h;
   return BA3C_OK;
 }
@@ -1126,7 +1128,7 @@ void ba3c_destroy(ba3c_handle* h) {
     if (e) (void)hipEventDestroy(e);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->side) (void)hipStreamDestroy(h->side);
-  if (h->bar) (void)hipFree(h->bar);
+  if (h->utag) (void)hipFree(h->utag);
   delete h;
 }
 
@@ -1268,18 +1270,19 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
   a.beta1 = hp->beta1;
   a.beta2 = hp->beta2;
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
-  if (fuse_clip && h->fused_update && h->bar && h->table.nchunks <= h->cus) {
+  if (fuse_clip && h->fused_update && h->utag && h->table.nchunks <= h->cus) {
     a.clip_part = part;
     const dim3 grid(h->table.nchunks);
+    const UpdateSync us{h->utag, reinterpret_cast<unsigned int*>(h->utag + h->table.nchunks)};
     {
       ProbeScope ps(h, s, BA3C_K_UPDATE);
       switch (opt) {
-        case BA3C_OPT_ADAM: hipLaunchKernelGGL(clip_update_kernel<0>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
-        case BA3C_OPT_GD: hipLaunchKernelGGL(clip_update_kernel<1>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
-        case BA3C_OPT_ADAGRAD: hipLaunchKernelGGL(clip_update_kernel<2>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
-        case BA3C_OPT_ADADELTA: hipLaunchKernelGGL(clip_update_kernel<3>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
-        case BA3C_OPT_MOMENTUM: hipLaunchKernelGGL(clip_update_kernel<4>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
-        case BA3C_OPT_RMS: hipLaunchKernelGGL(clip_update_kernel<5>, grid, dim3(256), 0, s, a, h->table, part, h->bar); break;
+        case BA3C_OPT_ADAM: hipLaunchKernelGGL(clip_update_kernel<0>, grid, dim3(256), 0, s, a, h->table, us); break;
+        case BA3C_OPT_GD: hipLaunchKernelGGL(clip_update_kernel<1>, grid, dim3(256), 0, s, a, h->table, us); break;
+        case BA3C_OPT_ADAGRAD: hipLaunchKernelGGL(clip_update_kernel<2>, grid, dim3(256), 0, s, a, h->table, us); break;
+        case BA3C_OPT_ADADELTA: hipLaunchKernelGGL(clip_update_kernel<3>, grid, dim3(256), 0, s, a, h->table, us); break;
+        case BA3C_OPT_MOMENTUM: hipLaunchKernelGGL(clip_update_kernel<4>, grid, dim3(256), 0, s, a, h->table, us); break;
+        case BA3C_OPT_RMS: hipLaunchKernelGGL(clip_update_kernel<5>, grid, dim3(256), 0, s, a, h->table, us); break;
         default: return fail(BA3C_ERR_INVALID, "unknown optimizer id");
       }
     }

@@ -558,63 +558,56 @@ __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const T
 // Fused clip_by_average_norm + optimizer apply in ONE launch (one workgroup per chunk, every
 // workgroup co-resident: gridDim.x = nchunks <= CUs).  Phase 1 loads the chunk's gradient,
 // parameters and slots and publishes its sum of squares (sumsq_kernel's order: the same
-// partials, bit for bit); a grid barrier; phase 2 is update_kernel's arithmetic with the clip
-// factor of the tensor.  The gradient is read once, the data loads overlap the barrier, and
-// the Adam beta powers on the device advance inside the barrier (no adam_powers launch).
+// partials, bit for bit) as a TAGGED word {generation, Σg²}; phase 2 waits only for the
+// partials of its own tensor (no grid-wide barrier, no atomics), forms the clip factor in
+// clip_factor's order and applies update_kernel's arithmetic.  The generation of chunk b is
+// the tag chunk b carried after the previous launch + 1: every launch runs every chunk, so
+// all tags advance in lockstep from the zeros ba3c_create wrote (graph replays included).
+// Cross-workgroup words go through agent-scope atomics (MI355X's 8 L2s are not coherent; a
+// __threadfence per workgroup costs an L2 write-back).  With device-resident Adam powers,
+// workgroup 0 advances them once every chunk has published (each reads them first).
+// Waits are bounded: a broken residency assumption cannot hang the device (err flag).
 // ---------------------------------------------------------------------------------------
-struct GridBarrier {
-  unsigned int count;   // arrivals of the running launch (reset by the last one)
-  unsigned int gen;     // generation: bumped by the last arrival
-  unsigned int err;     // 1: a wait gave up (bounded spin; results of that launch are invalid)
-  unsigned int pad;
+struct UpdateSync {
+  unsigned long long* tag;  // [nchunks] {generation << 32 | Σg² bits}
+  unsigned int* err;        // set when a wait gave up
 };
 
-
-// All workgroups of the grid meet here.  Every workgroup must be resident (the caller
-// guarantees gridDim.x <= CUs); the wait is bounded so a broken guarantee cannot hang the
-// device.  Data crossing the barrier must be written with st_agent and read with ld_agent
-// (device-coherent, no L2 write-back fence: an agent-scope __threadfence in each of ~90
-// workgroups cost more than the barrier saved).  Thread 0's s_waitcnt 0 completes its
-// st_agent before its arrival is counted.  `last` runs once, in the last workgroup to
-// arrive, before the others are released.
-template <class LastFn>
-__device__ __forceinline__ void grid_barrier(GridBarrier* b, LastFn&& last) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned g = __hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);
-    if (__hip_atomic_fetch_add(&b->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-      last();
-      __hip_atomic_store(&b->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-      __hip_atomic_store(&b->gen, g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      unsigned spins = 0;
-      while (__hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 22)) {
-          atomicOr(&b->err, 1u);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
+__device__ __forceinline__ unsigned long long ld_agent_u64(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// clip_factor over partials published with st_agent
-__device__ __forceinline__ float clip_factor_agent(const TensorTable& tt, int t, const float* part) {
+// wave 0 of the workgroup: wait until chunks [c0, c1) carry generation `gen`; returns the sum
+// of their partials in clip_factor's order (lane-strided, then the wave reduction)
+__device__ __forceinline__ float wait_partials(const UpdateSync& us, int c0, int c1, unsigned gen, int lane) {
   float ss = 0.f;
-  for (int b = tt.chunk0[t] + (int)(threadIdx.x & 63); b < tt.chunk0[t + 1]; b += 64) ss += ld_agent(part + b);
-  ss = wave_sum_f(ss);
-  return fminf(rsqrtf(ss) * (float)tt.numel[t], 10.0f);
+  for (int j0 = c0; j0 < c1; j0 += 64) {
+    const int j = j0 + lane;
+    unsigned long long w = 0;
+    unsigned spins = 0;
+    while (true) {
+      const bool ok = j >= c1 || (unsigned)((w = ld_agent_u64(us.tag + j)) >> 32) == gen;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {
+        if (lane == 0) atomicOr(us.err, 1u);
+        break;
+      }
+    }
+    if (j < c1) ss += __uint_as_float((unsigned)w);
+  }
+  return ss;
 }
 
 template <int OPT>
 __global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, const TensorTable tt,
-                                                          float* __restrict__ part, GridBarrier* bar) {
+                                                          const UpdateSync us) {
   __shared__ float red[4];
+  __shared__ float fsh;
   const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  // this launch's generation (issued first: its latency hides behind the data loads)
+  const unsigned gen = (unsigned)(ld_agent_u64(us.tag + b) >> 32) + 1u;
   const int t = table_find(tt, b);
   const int c = b - tt.chunk0[t];
   const int beg = c * UPD_CHUNK;
@@ -635,24 +628,32 @@ __global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, co
       if constexpr (S1) s1v[j] = a.s1[k];
     }
   }
+  float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1]) : a.alpha;
+  asm volatile("" : "+v"(alpha) : : "memory");   // the powers are read before this chunk publishes
   // phase 1: the chunk's sum of squares, in sumsq_kernel's order (i = beg + tid + 256 j)
   float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < PER; ++j)
     if (beg + (int)threadIdx.x + 256 * j < end) ss = fmaf(gv[j], gv[j], ss);
   ss = block_sum_256(ss, red);
-  if (threadIdx.x == 0) st_agent(part + b, ss);
-  float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1]) : a.alpha;
-  asm volatile("" : "+v"(alpha));    // the powers are read here, before this workgroup arrives
-  grid_barrier(bar, [&]() {
-    if (OPT == 0 && a.dev_powers) {   // every workgroup has read the powers before arriving
-      float* pw = const_cast<float*>(a.dev_powers);
-      pw[0] = pw[0] * a.beta1;
-      pw[1] = pw[1] * a.beta2;
+  if (threadIdx.x == 0)
+    __hip_atomic_store(us.tag + b, ((unsigned long long)gen << 32) | __float_as_uint(ss), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // phase 2: the tensor's clip factor (clip_factor's arithmetic) once its chunks published
+  if (threadIdx.x < 64) {
+    const float sum = wave_sum_f(wait_partials(us, tt.chunk0[t], tt.chunk0[t + 1], gen, lane));
+    if (lane == 0) fsh = fminf(rsqrtf(sum) * (float)tt.numel[t], 10.0f);
+    if (OPT == 0 && a.dev_powers && b == 0) {
+      (void)wait_partials(us, 0, gridDim.x, gen, lane);   // every chunk has read the powers
+      if (lane == 0) {
+        float* pw = const_cast<float*>(a.dev_powers);
+        pw[0] = pw[0] * a.beta1;
+        pw[1] = pw[1] * a.beta2;
+      }
     }
-  });
-  // phase 2: update_kernel's arithmetic (fused clip)
-  const float f = clip_factor_agent(tt, t, part);
+  }
+  __syncthreads();
+  const float f = fsh;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = beg + threadIdx.x + 256 * j;

@@ -44,9 +44,15 @@ struct Wg6Geom {
   static constexpr int KP = RB * WO;                      // output pixels of a full band
   static constexpr int KS = (KP + 31) / 32, KPAD = 32 * KS;
   static constexpr int XROWS = RB + KH - 1;
+  // RING: a workgroup that walks the bands of whole images keeps the 4 halo rows of band i as
+  // the first rows of band i + 1 and loads only RB new rows per band (halves X's HBM reads).
+  // Row groups of RB rows live in three LDS slots: group g in slot g & 1 and, for even g, also
+  // in slot 2, so the two groups (i, i + 1) a band reads are always contiguous from slot i & 1.
+  static constexpr bool RING = NBANDS > 1 && XROWS == 2 * RB;
+  static constexpr int XSLOTROWS = RING ? 3 * RB : XROWS;
   static constexpr int PX = PX_, PY = PY_;                // pixel pitches (bytes)
   static constexpr int XSB = 2 * CW, YSB = 2 * OW;        // bytes per split
-  static constexpr int X_BYTES = XROWS * WS * PX, Y_BYTES = KPAD * PY;
+  static constexpr int X_BYTES = XSLOTROWS * WS * PX, Y_BYTES = KPAD * PY;
   static constexpr int NCG = CIN / CW, NOG = COUT / OW;
   static constexpr int TBASE = NTAP / 4, TREM = NTAP % 4;  // taps per wave: 7, 6, 6, 6
   static constexpr int TW = TBASE + (TREM > 0);
@@ -104,18 +110,35 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
   uint32_t yc[YPT];                                       // (un-loaded: dY is zero)
 
   const int nbands = a.batch * G::NBANDS;
+  // band walk: whole images per workgroup (ring reuse of the halo rows) when every workgroup
+  // gets at least one image, else bands bx, bx + gx, ... (small batches)
+  const bool ring = G::RING && a.batch >= gx;
+  int band_end = nbands;
+  int band = bx;
+  if (ring) {
+    const int ipw = (a.batch + gx - 1) / gx;
+    band = min(a.batch, bx * ipw) * G::NBANDS;
+    band_end = min(a.batch, (bx + 1) * ipw) * G::NBANDS;
+  }
+  const int bstep = ring ? 1 : gx;
+  // rows [r0, XROWS) of the band's input window: all of them, or (ring, not the image's first
+  // band) only the RB rows that are new
+  int xr0 = 0;
   auto load_band = [&](int band) {
     const int img = band / G::NBANDS;
-    const int y0 = (band - img * G::NBANDS) * G::RB;
+    const int bi = band - img * G::NBANDS;
+    const int y0 = bi * G::RB;
     const int rows_out = min(G::RB, G::HO - y0);
+    xr0 = (ring && bi > 0) ? G::RB : 0;
+    const int xn = (G::XROWS - xr0) * G::WS * XQ;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int f = tid + 256 * i;
       const int pix = f / XQ, cq = f - pix * XQ;
-      const int ry = pix / G::WS, x = pix - ry * G::WS;
+      const int ry = xr0 + pix / G::WS, x = pix - (pix / G::WS) * G::WS;
       const int y = y0 + ry;
       xv[i] = f4zero();
-      if (f < XN && y < G::HS)
+      if (f < xn && y < G::HS)
         xv[i] = *reinterpret_cast<const float4*>(a.x + ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + c0 + cq * 4);
     }
 #pragma unroll
@@ -134,19 +157,31 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
     }
   };
   auto store_band = [&](int band) {
-    const int y0 = (band - (band / G::NBANDS) * G::NBANDS) * G::RB;
+    const int bi = band - (band / G::NBANDS) * G::NBANDS;
+    const int y0 = bi * G::RB;
+    const int xn = (G::XROWS - xr0) * G::WS * XQ;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int f = tid + 256 * i;
-      if (f < XN) {
+      if (f < xn) {
         const int pix = f / XQ, cq = f - pix * XQ;
+        const int ry = xr0 + pix / G::WS, x = pix - (pix / G::WS) * G::WS;
         uint32_t s0[G::NS], s1[G::NS];
         SP::split(xv[i].x, xv[i].y, xsc, s0);
         SP::split(xv[i].z, xv[i].w, xsc, s1);
-        char* p = xs + pix * G::PX + cq * 8;
+        // window row ry of band bi is row ry % RB of group bi + ry / RB
+        const int g = bi + ry / G::RB, rr = ry - (ry / G::RB) * G::RB;
+        const int prow = ring ? (g & 1) * G::RB + rr : ry;
+        char* p = xs + (prow * G::WS + x) * G::PX + cq * 8;
 #pragma unroll
         for (int sp = 0; sp < G::NS; ++sp)
           *reinterpret_cast<uint2*>(p + sp * G::XSB) = make_uint2(s0[sp], s1[sp]);
+        if (ring && (g & 1) == 0) {                       // even groups also in slot 2
+          char* q = p + 2 * G::RB * G::WS * G::PX;
+#pragma unroll
+          for (int sp = 0; sp < G::NS; ++sp)
+            *reinterpret_cast<uint2*>(q + sp * G::XSB) = make_uint2(s0[sp], s1[sp]);
+        }
       }
     }
 #pragma unroll
@@ -170,16 +205,18 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
     }
   };
 
-  int band = bx;
-  if (band < nbands) load_band(band);
-  for (; band < nbands; band += gx) {
+  if (band < band_end) load_band(band);
+  for (; band < band_end; band += bstep) {
     const int img = band / G::NBANDS;
-    const int rows_out = min(G::RB, G::HO - (band - img * G::NBANDS) * G::RB);
+    const int bi = band - img * G::NBANDS;
+    const int rows_out = min(G::RB, G::HO - bi * G::RB);
     const int kvalid = rows_out * G::WO;
+    // first window row of this band in the X slots (ring: slot bi & 1)
+    const int xbase = ring ? (bi & 1) * G::RB * G::WS * G::PX : 0;
     __syncthreads();                                      // previous band's LDS reads done
     store_band(band);
     __syncthreads();
-    if (band + gx < nbands) load_band(band + gx);
+    if (band + bstep < band_end) load_band(band + bstep);
 
 #pragma unroll 1
     for (int s = 0; s < G::KS; ++s) {
@@ -191,7 +228,7 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
         yb[r] = p * G::PY + 8 * pq;
         if (p >= kvalid) p = 0;                           // padded pixels: dY is zero
         const int y = p / G::WO, x = p - y * G::WO;
-        xb[r] = (y * G::WS + x) * G::PX + 8 * pq;
+        xb[r] = xbase + (y * G::WS + x) * G::PX + 8 * pq;
       }
       u32x4 b[2][G::NS];
 #pragma unroll

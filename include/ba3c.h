@@ -1,10 +1,13 @@
 /*
  * ba3c.h — C ABI of the MI355X-native BA3C learner/predictor hot path (libba3c.so).
  *
- * Plain pointers and sizes only: every device buffer is owned by the caller (the Python
- * host allocates them with PyTorch-ROCm); the handle owns only static configuration and
- * a few HIP events.  No call allocates device memory, none synchronises the stream except
- * ba3c_probe_read, and none throws: every entry returns a BA3C_* status and
+ * Plain pointers and sizes only: every data buffer is owned by the caller (the Python
+ * host allocates them with PyTorch-ROCm); the handle owns static configuration, a few HIP
+ * events and 16 bytes of device memory allocated by ba3c_create (the grid-barrier words of
+ * the fused clip + optimizer launch; without a device they stay unallocated and the apply
+ * uses two launches).  One handle serves one stream at a time.  No other call allocates
+ * device memory, none synchronises the stream except ba3c_probe_read, and none throws:
+ * every entry returns a BA3C_* status and
  * ba3c_last_error() holds a thread-local message.  All device pointers must be 16-byte
  * aligned.  `stream` is a hipStream_t (NULL = default stream).
  *
@@ -144,8 +147,10 @@ int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace)
 
 /* One optimizer apply over the flat buffers: g_eff = grads*grad_scale (1/world after an
  * all-reduce-sum), or, with fuse_clip=1, clip_by_average_norm(grads) fused in (single
- * replica).  slot0/slot1: Adam m/v, RMS ms/mom, Adagrad accum, Adadelta accum/accum_update,
- * Momentum accum; unused slots may be NULL. */
+ * replica; one launch with a grid barrier when the tensor chunks fit one workgroup per CU,
+ * bit-identical to ba3c_clip_grads followed by an unfused apply).  slot0/slot1: Adam m/v,
+ * RMS ms/mom, Adagrad accum, Adadelta accum/accum_update, Momentum accum; unused slots may
+ * be NULL. */
 int ba3c_apply_update(ba3c_handle* h, void* stream, int32_t opt, float* params,
                       const float* grads, float* slot0, float* slot1,
                       const ba3c_opt_params* hp, float grad_scale, int32_t fuse_clip,
