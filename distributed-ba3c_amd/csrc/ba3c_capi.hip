@@ -99,6 +99,11 @@ struct ba3c_handle {
   // joined by events (r02k trace at B=32: 6-11 us of idle queue per fork / join).
   // BA3C_MULTI=0: side stream as before.
   bool multi = true;
+  // fc1 + heads backward as one multi-job launch at batches > OVERLAP_B too (BA3C_MULTI_BIG=0:
+  // off): r02x at B=2048, 84 -> 64 us for the three products.  conv3's pair measured slower
+  // there (116 -> 134 us) and conv1 / conv2 each fill the chip (and the dominant kernel's
+  // roofline probe needs it on its own), so they keep one kernel per product above OVERLAP_B.
+  int multi_big = 1;
   // fused-clip optimizer applies as one clip_update_kernel launch (ba3c_small.h) when the chunk
   // count fits one workgroup per CU; its grid-barrier words live in `bar` (device, zeroed at
   // create).  BA3C_FUSED_UPDATE=0: sumsq_kernel + update_kernel.
@@ -404,7 +409,8 @@ Band6Args band6_args(ba3c_handle* h, const BandArgs& a, const Workspace& w, int 
 // register budget of the band / weight-gradient kernels; T512: 512-thread jobs.
 template <bool W2, class J0, class J1, class J2 = NoJob, bool T512 = false>
 int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const typename J1::Args& a1, dim3 g1,
-                 const typename J2::Args& a2 = typename J2::Args{}, dim3 g2 = dim3(0, 1, 1)) {
+                 const typename J2::Args& a2 = typename J2::Args{}, dim3 g2 = dim3(0, 1, 1),
+                 ba3c_handle* h = nullptr, int kid = -1) {
   MultiGrid g;
   const dim3 gs[3] = {g0, g1, g2};
   int end = 0;
@@ -415,6 +421,12 @@ int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const type
     g.end[j] = end;
   }
   if (end == 0) return BA3C_OK;
+  // the timing probe brackets the whole launch under job 0's kernel id
+  struct OptProbe {
+    ProbeScope* p = nullptr;
+    ~OptProbe() { delete p; }
+  } probe;
+  if (h && kid >= 0) probe.p = new ProbeScope(h, s, kid);
   if constexpr (T512)
     hipLaunchKernelGGL((multi_kernel512<J0, J1, J2>), dim3(end), dim3(512), 0, s, a0, a1, a2, g);
   else if constexpr (W2)
@@ -745,10 +757,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // small batches on the split path: each layer's input- and weight-gradient kernels as one
   // multi-job launch on `s` (no side stream, no events); otherwise the side stream joins a
   // graph capture of `s` through the fork events
-  const bool mj = h->multi && h->overlap != 1 && B <= OVERLAP_B && h->band && h->b6 && h->w6 && h->g6 &&
-                  h->split && CH == 4;
+  const bool mjok = h->multi && h->overlap != 1 && h->band && h->b6 && h->w6 && h->g6 && h->split && CH == 4;
+  const bool mj = mjok && B <= OVERLAP_B;
+  const bool mj_fc = mj || (mjok && (h->multi_big & 1));
+
   static_assert(OVERLAP_B <= SMALL_B, "multi-job conv2 input gradient is the small-batch geometry");
   if (!mj && h->side && (h->overlap == 1 || B <= OVERLAP_B)) ws = h->side;
+  const bool big = B > OVERLAP_B;   // multi-job gemm jobs: 2-deep k-tile rings (full grids)
   // every weight-gradient reduction is deferred into one launch at the end (RAII: an early
   // error return leaves the handle in immediate mode)
   struct DeferGuard {
@@ -769,11 +784,14 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     WgradPlan plf = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
     BatchWgrad gf{w.a3, w.dh, w.part_f, 1600, F, legacy ? 1 : 0, plf.M, plf.N, plf.K, plf.kchunk};
     FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
-    if (mj)   // fc1 input gradient + head and fc1 weight gradients: one launch
+    const dim3 gd((d.M + 63) / 64, (d.N + 63) / 64, 1), gh((pl.M + 127) / 128, (pl.N + 31) / 32, pl.S),
+        gff((plf.M + 127) / 128, (plf.N + 63) / 64, plf.S);
+    if (mj_fc && !big)   // fc1 input gradient + head and fc1 weight gradients: one launch
       CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, 4>, Gemm6Job<128, 32, 4, 1, BatchWgrad, 4>,
-                          Gemm6Job<128, 64, 2, 2, BatchWgrad, 4>>(
-          s, d, dim3((d.M + 63) / 64, (d.N + 63) / 64, 1), g, dim3((pl.M + 127) / 128, (pl.N + 31) / 32, pl.S), gf,
-          dim3((plf.M + 127) / 128, (plf.N + 63) / 64, plf.S))));
+                          Gemm6Job<128, 64, 2, 2, BatchWgrad, 4>>(s, d, gd, g, gh, gf, gff, h, BA3C_K_FC1_DGRAD)));
+    else if (mj_fc)
+      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, 2>, Gemm6Job<128, 32, 4, 1, BatchWgrad, 2>,
+                          Gemm6Job<128, 64, 2, 2, BatchWgrad, 2>>(s, d, gd, g, gh, gf, gff, h, BA3C_K_FC1_DGRAD)));
     else
       CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_HEAD_WGRAD, g, pl.S)));
     ReduceMap mp{};
@@ -791,7 +809,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   {
     WgradPlan pl = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
     BatchWgrad g{w.a3, w.dh, w.part_f, 1600, F, legacy ? 1 : 0, pl.M, pl.N, pl.K, pl.kchunk};
-    if (!mj) CHECK((launch_gemm<128, 64, 2, 2>(h, ws, BA3C_K_FC1_WGRAD, g, pl.S)));
+    if (!mj_fc) CHECK((launch_gemm<128, 64, 2, 2>(h, ws, BA3C_K_FC1_WGRAD, g, pl.S)));
     ReduceMap mp{};
     mp.kind = 1;
     mp.M = pl.M;
@@ -804,7 +822,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // fc1 input gradient -> dY3 (ReluGrad of conv3 fused)
   {
     FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
-    if (!mj) CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
+    if (!mj_fc) CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
     CHECK(fork());
   }
   auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad, const float* part) {
@@ -823,17 +841,17 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0,
                                            NS == 2 ? w.am(AM_DP2, h) : nullptr};
-    // The input gradient's K = 576 runs in two halves summed in the workgroup (KS = 2) at
-    // every batch (each image's dP2 rounds the same in any batch, like the forward); the
-    // weight gradient takes KS = 2 for B <= OVERLAP_B on every launch path (the multi-job
-    // and side-stream paths give the same bits)
+    // The input gradient splits its k-tiles over two wave groups of a 512-thread workgroup
+    // (KS = 2) at every batch (each image's dP2 rounds the same in any batch, like the
+    // forward); the weight gradient does for B <= OVERLAP_B (r02x: KS = 2 at B=2048 35 -> 45 us),
+    // on every launch path, so the multi-job and separate launches agree bit for bit
+    const dim3 gd((d.M + 63) / 64, (d.N + 63) / 64, 1), gw((pl.M + 127) / 128, (pl.N + 63) / 64, pl.S);
     if (mj) {
       CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, decltype(d), 4, 2>, Gemm6Job<128, 64, 4, 1, decltype(g), 4, 2>,
-                          NoJob, true>(
-          s, d, dim3((d.M + 63) / 64, (d.N + 63) / 64, 1), g, dim3((pl.M + 127) / 128, (pl.N + 63) / 64, pl.S))));
+                          NoJob, true>(s, d, gd, g, gw, 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
     } else {
-      if (B <= OVERLAP_B) CHECK((launch_gemm<128, 64, 4, 1, decltype(g), 2>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
-      else CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
+      if (big) CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
+      else CHECK((launch_gemm<128, 64, 4, 1, decltype(g), 2>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
       CHECK((launch_gemm<64, 64, 2, 2, decltype(d), 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
     }
     CHECK(conv_reduce(pl, 3, 64, 64, w.part_3));
@@ -1034,6 +1052,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
   if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
+  if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 1;
   if (const char* e = getenv("BA3C_FUSED_UPDATE")) h->fused_update = !(e[0] == '0');
   if (const char* e = getenv("BA3C_PIPE")) h->pipe = (e[0] == '1');
   {

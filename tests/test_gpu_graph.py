@@ -98,3 +98,29 @@ def test_backward_launch_paths_match_single_stream(monkeypatch, mode):
     for s_cap, s_ref in zip(cap.optimizer.slots, ref.optimizer.slots):
         np.testing.assert_array_equal(s_cap.cpu().numpy(), s_ref.cpu().numpy())
     assert cap.optimizer.powers() == ref.optimizer.powers()
+
+
+def test_large_batch_fc1_multi_job_matches_separate_launches(monkeypatch):
+    """Above OVERLAP_B the fc1 input gradient and the head / fc1 weight gradients run as one
+    multi-job launch (default) or as three launches (BA3C_MULTI_BIG=0): same gradients and
+    scalars bit for bit (B=160, F=512, S=1: the bench geometry)."""
+    from ba3c_amd.engine import Ba3cEngine
+    B = 160
+    rs = np.random.RandomState(77)
+    state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    params = O.init_params(512, 1, 4, seed=7, dtype=np.float32)
+    out = []
+    for env in ("0", None):
+        if env is None:
+            monkeypatch.delenv("BA3C_MULTI_BIG", raising=False)
+        else:
+            monkeypatch.setenv("BA3C_MULTI_BIG", env)
+        eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=B)
+        eng.load_params(params)
+        sc = eng.train_grads(state, action, R)
+        torch.cuda.synchronize()
+        out.append((eng.grads.clone(), sc.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
