@@ -363,7 +363,8 @@ int launch_reduce(ba3c_handle* h, hipStream_t s, const float* part, int S, const
     j.S[j.n] = S;
     j.mp[j.n] = mp;
     const int no = mp.kind == 0 ? (mp.M / mp.cin) * mp.cinpad * mp.N : mp.M * mp.N;
-    j.blk0[j.n + 1] = j.blk0[j.n] + (no + 63) / 64;
+    j.vec[j.n] = reduce_vec_ok(mp) ? 1 : 0;
+    j.blk0[j.n + 1] = j.blk0[j.n] + (no + (j.vec[j.n] ? 255 : 63)) / (j.vec[j.n] ? 256 : 64);
     ++j.n;
     return BA3C_OK;
   }

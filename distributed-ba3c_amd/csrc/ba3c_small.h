@@ -336,7 +336,14 @@ struct ReduceJobs {
   int S[MAX_RJOBS];
   ReduceMap mp[MAX_RJOBS];
   int blk0[MAX_RJOBS + 1];
+  int vec[MAX_RJOBS];   // 1: four consecutive outputs per lane (float4 slab loads / stores)
 };
+
+// a job can take float4 lanes when its output rows are whole float4s in the partial slabs
+// and in the destination (conv HWIO / fc1 split layouts with N % 4 == 0)
+__host__ __device__ inline bool reduce_vec_ok(const ReduceMap& mp) {
+  return mp.kind != 2 && mp.N % 4 == 0 && (mp.kind == 0 || mp.per % 4 == 0);
+}
 
 __device__ __forceinline__ int reduce_out_size(const ReduceMap& mp) {
   return mp.kind == 0 ? (mp.M / mp.cin) * mp.cinpad * mp.N : mp.M * mp.N;
@@ -344,6 +351,7 @@ __device__ __forceinline__ int reduce_out_size(const ReduceMap& mp) {
 
 __global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs jobs) {
   __shared__ float red[4][64];
+  __shared__ float4 red4[4][64];
   const int b = blockIdx.x;
   int j = 0;
   while (j + 1 < jobs.n && jobs.blk0[j + 1] <= b) ++j;
@@ -352,6 +360,62 @@ __global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs 
   const int S = jobs.S[j];
   const int lane = threadIdx.x & 63, zg = threadIdx.x >> 6;
   const int MN = mp.M * mp.N;
+  if (jobs.vec[j]) {
+    // 256 outputs per workgroup, 4 consecutive per lane: the per-output sums are the scalar
+    // path's (z mod 4 lane groups in z order, then ((s0 + s1) + s2) + s3), bit for bit
+    const int o = ((b - jobs.blk0[j]) * 64 + lane) * 4;
+    const int NO = reduce_out_size(mp);
+    int po = o;
+    if (mp.kind == 0 && mp.cinpad != mp.cin && o < NO) {
+      const int n = o % mp.N, r = o / mp.N, kk = r / mp.cinpad, c = r - kk * mp.cinpad;
+      po = c < mp.cin ? (kk * mp.cin + c) * mp.N + n : -1;
+    }
+    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (o < NO && po >= 0) {
+      const float4* __restrict__ p4 = reinterpret_cast<const float4*>(part);
+      const int MN4 = MN / 4, q = po / 4;
+      int z = zg;
+      for (; z + 28 < S; z += 32) {
+        float4 a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = p4[(size_t)(z + 4 * u) * MN4 + q];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          sv.x += a[u].x;
+          sv.y += a[u].y;
+          sv.z += a[u].z;
+          sv.w += a[u].w;
+        }
+      }
+      for (; z < S; z += 4) {
+        const float4 a = p4[(size_t)z * MN4 + q];
+        sv.x += a.x;
+        sv.y += a.y;
+        sv.z += a.z;
+        sv.w += a.w;
+      }
+    }
+    red4[zg][lane] = sv;
+    __syncthreads();
+    if (zg == 0 && o < NO) {
+      const float4 r0 = red4[0][lane], r1 = red4[1][lane], r2 = red4[2][lane], r3 = red4[3][lane];
+      float4 v;
+      v.x = ((r0.x + r1.x) + r2.x) + r3.x;
+      v.y = ((r0.y + r1.y) + r2.y) + r3.y;
+      v.z = ((r0.z + r1.z) + r2.z) + r3.z;
+      v.w = ((r0.w + r1.w) + r2.w) + r3.w;
+      if (po < 0) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      float* dst;
+      if (mp.kind == 0) {
+        dst = mp.dst + o;                                   // [(kk * cinpad + c) * N + n] == o
+      } else {
+        const int m = o / mp.N, n = o % mp.N, sidx = n / mp.per, fl = n - sidx * mp.per;
+        dst = mp.dst + (size_t)sidx * mp.wstride + (size_t)m * mp.per + fl;
+      }
+      *reinterpret_cast<float4*>(dst) = v;
+    }
+    return;
+  }
   const int o = (b - jobs.blk0[j]) * 64 + lane;            // output element of the job
   const int NO = reduce_out_size(mp);
   int po = o;                                               // its partial index, -1: padding
