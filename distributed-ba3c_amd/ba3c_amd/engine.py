@@ -223,6 +223,12 @@ class Ba3cEngine(object):
         """3: bf16 split planes, 2: scaled fp16 split planes, else kernel_split's value."""
         return int(self.lib.ba3c_kernel_family(self.h, _lib.KERNEL_IDS[kernel]))
 
+    def device_errors(self):
+        """Error flags of the handle's in-launch waits (0 = none; synchronises the device)."""
+        f = ctypes.c_uint32()
+        _lib.check(self.lib.ba3c_device_errors(self.h, ctypes.byref(f)))
+        return f.value
+
     def probe_read(self):
         ms, n = ctypes.c_double(), ctypes.c_int32()
         _lib.check(self.lib.ba3c_probe_read(self.h, ctypes.byref(ms), ctypes.byref(n)))

@@ -99,11 +99,11 @@ struct ba3c_handle {
   // joined by events (r02k trace at B=32: 6-11 us of idle queue per fork / join).
   // BA3C_MULTI=0: side stream as before.
   bool multi = true;
-  // fc1 + heads backward as one multi-job launch at batches > OVERLAP_B too (BA3C_MULTI_BIG=0:
-  // off): r02x at B=2048, 84 -> 64 us for the three products.  conv3's pair measured slower
-  // there (116 -> 134 us) and conv1 / conv2 each fill the chip (and the dominant kernel's
-  // roofline probe needs it on its own), so they keep one kernel per product above OVERLAP_B.
-  int multi_big = 1;
+  // Backward pairs run as multi-job launches at batches > OVERLAP_B too (BA3C_MULTI_BIG bits:
+  // 1 fc1 + heads — r02x at B=2048, 84 -> 64 us for the three products; 2 conv2 — r02aa, 300 ->
+  // 292 us).  conv3's pair measured slower there (116 -> 134 us), and conv1's products stay
+  // on their own (the dominant kernel's roofline probe needs conv1 dgrad alone).
+  int multi_big = 3;
   // fused-clip optimizer applies as one clip_update_kernel launch (ba3c_small.h) when the chunk
   // count fits one workgroup per CU; its grid-barrier words live in `bar` (device, zeroed at
   // create).  BA3C_FUSED_UPDATE=0: sumsq_kernel + update_kernel.
@@ -761,6 +761,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   const bool mjok = h->multi && h->overlap != 1 && h->band && h->b6 && h->w6 && h->g6 && h->split && CH == 4;
   const bool mj = mjok && B <= OVERLAP_B;
   const bool mj_fc = mj || (mjok && (h->multi_big & 1));
+  const bool mj_c2 = !mj && mjok && (h->multi_big & 2);   // large-batch conv2 pair (A/B: BA3C_MULTI_BIG=3)
 
   static_assert(OVERLAP_B <= SMALL_B, "multi-job conv2 input gradient is the small-batch geometry");
   if (!mj && h->side && (h->overlap == 1 || B <= OVERLAP_B)) ws = h->side;
@@ -866,6 +867,14 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
                                                       w, WT_C2D, SplitIO{AM_DP2, 3, AM_DP1});
     CHECK((launch_multi<true, Band6Job<typename LY::C2DS>, Wg6Job<typename LY::W2>>(
         s, da, dim3(B * LY::C2DS::G::NBANDS), wa, wg)));
+    CHECK(reduce_wgrad6<typename LY::W2>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[2]].offset));
+  } else if (mj_c2) {
+    const Wg6Args wa{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)};
+    const dim3 wg = wgrad6_grid<typename LY::W2>(W6_P2, B);
+    const Band6Args da = band6_args<typename LY::C2D>(h, BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B},
+                                                     w, WT_C2D, SplitIO{AM_DP2, 3, AM_DP1});
+    CHECK((launch_multi<true, Band6Job<typename LY::C2D>, Wg6Job<typename LY::W2>>(
+        s, da, dim3(B * LY::C2D::G::NBANDS), wa, wg, 0, dim3(0, 1, 1), h, BA3C_K_CONV2_DGRAD)));
     CHECK(reduce_wgrad6<typename LY::W2>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[2]].offset));
   } else {
     if (h->band && h->w6) {
@@ -1053,7 +1062,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
   if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 1;
+  if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 3;
   if (const char* e = getenv("BA3C_FUSED_UPDATE")) h->fused_update = !(e[0] == '0');
   if (const char* e = getenv("BA3C_PIPE")) h->pipe = (e[0] == '1');
   {
@@ -1481,6 +1490,16 @@ int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {
   if (kid == BA3C_K_CONV0_FWD || kid == BA3C_K_CONV0_WGRAD)
     if (!(h->band && h->cfg.channels == 4 && h->split)) return 3;
   return band_split && h->ns == 2 ? 2 : 3;
+}
+
+int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
+  if (!h || !flags) return fail(BA3C_ERR_INVALID, "null argument");
+  *flags = 0;
+  if (!h->utag) return BA3C_OK;
+  uint32_t e = 0;
+  HIP_TRY(hipMemcpy(&e, h->utag + h->table.nchunks, sizeof(e), hipMemcpyDeviceToHost));
+  *flags = e;
+  return BA3C_OK;
 }
 
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches) {

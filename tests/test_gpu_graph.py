@@ -98,6 +98,8 @@ def test_backward_launch_paths_match_single_stream(monkeypatch, mode):
     for s_cap, s_ref in zip(cap.optimizer.slots, ref.optimizer.slots):
         np.testing.assert_array_equal(s_cap.cpu().numpy(), s_ref.cpu().numpy())
     assert cap.optimizer.powers() == ref.optimizer.powers()
+    for tr in (ref, eager, cap):
+        assert tr.engine.device_errors() == 0      # no in-launch wait gave up
 
 
 def test_large_batch_fc1_multi_job_matches_separate_launches(monkeypatch):
