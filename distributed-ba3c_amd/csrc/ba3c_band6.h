@@ -328,6 +328,67 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
   band6_body<L>(a, blockIdx.x, reinterpret_cast<char*>(lds4));
 }
 
+// Ring-walk persistent variant (NPH == 1 layouts, large batches): each workgroup walks the
+// bands of whole images in order.  Band i + 1's first KH - 1 input rows are band i's last ones,
+// already split in LDS: they move down with one LDS-to-LDS copy (rows RB .. SROWS-1 -> 0 ..
+// KH-2, disjoint ranges) and only the RB new rows are loaded, un-pooled and split — the
+// band's staging VALU and global reads drop by (KH - 1) / SROWS (40 % for conv1 fwd's 6-row
+// bands, 50 % for conv1 dgrad's 4-row ones).  Per band the LDS image and the MFMA stream are
+// the one-band kernel's, so the outputs are bit-identical.
+template <class L>
+__device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, char* lds) {
+  static_assert(L::NPH == 1 && L::G::SROWS > L::G::RB, "ring walk: unphased layouts with a halo");
+  using O = Band6Ops<L>;
+  using G = typename L::G;
+  constexpr int HALO = G::SROWS - G::RB;                    // KH - 1 rows carried over
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
+  const int ipw = (a.batch + gx - 1) / gx;
+  const int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
+  unsigned long long pos = 0;
+  for (int img = img0; img < img1; ++img) {
+    const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
+    const float asc = exp2i(ka), us1 = exp2i(-ka);
+    float omax = 0.f;
+    for (int bi = 0; bi < G::NBANDS; ++bi) {
+      const int y0 = bi * G::RB;
+      const int rows_out = min(G::RB, G::HO - y0);
+      __syncthreads();                                      // previous band's LDS reads are done
+      unsigned fbase = 0;
+      if (bi > 0) {
+        // carry the halo rows down (disjoint source / destination rows)
+        constexpr int N16 = HALO * L::RP / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(lds + G::RB * L::RP);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+        for (int i = tid; i < N16; i += 256) dst[i] = src[i];
+        fbase = (unsigned)HALO * G::WS * O::Q;              // stage rows HALO .. SROWS-1 only
+      }
+      // staging of rows [fbase / (WS Q), rows_out + KH - 1), loads in chunks, then the stores
+      const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * O::Q;
+      constexpr int NPT = O::NTOT < BA3C_STAGE_NPT ? O::NTOT : BA3C_STAGE_NPT;
+      for (unsigned base = fbase; base < nvec; base += 256u * NPT) {
+        float4 v[NPT];
+        uint32_t cd[NPT];
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) O::load1(a, img, y0, rows_out, 0, base + tid + 256u * i, v[i], cd[i]);
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) O::store1(lds, y0, rows_out, base + tid + 256u * i, v[i], cd[i], asc);
+      }
+      __syncthreads();
+      O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [](int) {});
+    }
+    if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
+  }
+  if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
+}
+
+template <class L>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6r_kernel(const Band6Args a) {
+  __shared__ uint4 lds4[L::LDS_BYTES / 16];
+  band6r_body<L>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
+}
+
 // Pipelined persistent variant (NPH == 1 layouts): one 512-thread workgroup per CU walks
 // bands blockIdx.x, + gridDim.x, ...; waves 4..7 stage band i + 1 into one of two LDS
 // buffers while waves 0..3 run band i's MFMAs from the other, one barrier per band.  The

@@ -77,6 +77,9 @@ struct ba3c_handle {
   // measured it slower (conv1 fwd 0.41 -> 0.51 ms, dgrad 0.43 -> 0.47 ms) — one compute wave
   // per SIMD exposes the LDS-read latency that two co-resident one-band workgroups hide.
   bool pipe = false;
+  // conv1 fwd / dgrad (multi-band layouts) as ring-walk persistent kernels at batches that
+  // give every workgroup whole images (conv_band6r_kernel; BA3C_RING=0: one band per workgroup)
+  bool ring = true;
   int cus = 256;      // compute units of the device (persistent grids)
   int c0lay = 2;      // conv0 forward LDS layout (ba3c_split.h; BA3C_C0LAY=0/1/2)
   bool g6 = true;     // implicit-GEMM launches (conv3, fc1, heads; C=12 conv0) on bf16x6 split
@@ -447,6 +450,13 @@ int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, cons
   const int nbands = a.batch * L::G::NBANDS;
   {
     ProbeScope ps(h, s, kid);
+    if constexpr (L::NPH == 1 && L::G::NBANDS > 1 && L::G::SROWS > L::G::RB) {
+      if (pipelined && h->ring && a.batch >= 2 * h->cus) {
+        hipLaunchKernelGGL(conv_band6r_kernel<L>, dim3(2 * h->cus), dim3(256), 0, s, b);
+        HIP_TRY(hipGetLastError());
+        return BA3C_OK;
+      }
+    }
     if constexpr (LP::NPH == 1 && 2 * LP::LDS_BYTES <= 160 * 1024) {
       if (pipelined && h->pipe && nbands >= 4 * h->cus) {
         hipLaunchKernelGGL(conv_band6p_kernel<LP>, dim3(std::min(nbands, h->cus)), dim3(512), 0, s, b);
@@ -1065,6 +1075,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 3;
   if (const char* e = getenv("BA3C_FUSED_UPDATE")) h->fused_update = !(e[0] == '0');
   if (const char* e = getenv("BA3C_PIPE")) h->pipe = (e[0] == '1');
+  if (const char* e = getenv("BA3C_RING")) h->ring = !(e[0] == '0');
   {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess &&

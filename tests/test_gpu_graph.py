@@ -126,3 +126,32 @@ def test_large_batch_fc1_multi_job_matches_separate_launches(monkeypatch):
         out.append((eng.grads.clone(), sc.clone()))
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
+
+
+def test_ring_walk_band_kernels_match_one_band_kernels(monkeypatch):
+    """From B = 2 x CUs up, conv1's forward and input gradient run as ring-walk persistent
+    kernels (whole images per workgroup, halo rows carried in LDS) instead of one band per
+    workgroup (BA3C_RING=0): activations, dp0, gradients and scalars bit for bit equal."""
+    from ba3c_amd.engine import Ba3cEngine
+    B = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    rs = np.random.RandomState(78)
+    state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    params = O.init_params(512, 1, 4, seed=8, dtype=np.float32)
+    out = []
+    for env in ("0", None):
+        if env is None:
+            monkeypatch.delenv("BA3C_RING", raising=False)
+        else:
+            monkeypatch.setenv("BA3C_RING", env)
+        eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=B)
+        eng.load_params(params)
+        sc = eng.train_grads(state, action, R)
+        ws = {n: eng.workspace_tensor(n, B).clone() for n in ("p1", "c1", "dp0")}
+        torch.cuda.synchronize()
+        out.append((eng.grads.clone(), sc.clone(), ws))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    for n in out[0][2]:
+        assert torch.equal(out[0][2][n], out[1][2][n]), n
