@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -426,11 +427,8 @@ int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const type
   }
   if (end == 0) return BA3C_OK;
   // the timing probe brackets the whole launch under job 0's kernel id
-  struct OptProbe {
-    ProbeScope* p = nullptr;
-    ~OptProbe() { delete p; }
-  } probe;
-  if (h && kid >= 0) probe.p = new ProbeScope(h, s, kid);
+  std::optional<ProbeScope> probe;
+  if (h && kid >= 0) probe.emplace(h, s, kid);
   if constexpr (T512)
     hipLaunchKernelGGL((multi_kernel512<J0, J1, J2>), dim3(end), dim3(512), 0, s, a0, a1, a2, g);
   else if constexpr (W2)

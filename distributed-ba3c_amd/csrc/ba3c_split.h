@@ -414,6 +414,15 @@ __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
 // s = wave, wave + 4, ...  The next band's global loads are issued into registers before
 // the MFMA phase of the current one.  Each workgroup writes one partial slab (x 1/255).
 // ---------------------------------------------------------------------------------------
+// A-row slot -> tap of conv0's weight gradient (7 m-tiles x 4 slots; see Conv0W's pitches):
+// C0W_TAP_ADDR is the tap whose pixels a slot reads, C0W_TAP_OUT the tap it computes (-1:
+// padding, discarded).  A slot's MFMA row is independent of the others, so the order changes
+// nothing in any output's arithmetic.
+__device__ constexpr int C0W_TAP_ADDR[28] = {0, 2, 1, 3, 8, 5, 4, 6, 11, 13, 7, 9, 14, 16,
+                                             10, 12, 17, 19, 18, 15, 20, 22, 21, 23, 0, 2, 24, 3};
+__device__ constexpr int C0W_TAP_OUT[28] = {0, 2, 1, 3, 8, 5, 4, 6, 11, 13, 7, 9, 14, 16,
+                                            10, 12, 17, 19, 18, 15, 20, 22, 21, 23, -1, -1, 24, -1};
+
 template <int NS>
 struct Conv0W {
   static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
@@ -425,12 +434,17 @@ struct Conv0W {
   static constexpr int KSW = KSTEPS / 4;           // 5 per wave
   static constexpr int Y_16 = NS * PRB * COUT * PW;                   // 16-bit words
   static constexpr int YC_BYTES = PRB * COUT * PW;                    // 5120
-  // row / channel-plane / copy pitches (16-bit units) from a bank search over the A-fragment
-  // dword reads (2 x 32-lane groups, bank mod 32): 1.43 LDS cycles per read against 3.71 for
-  // the dense 88 / 1056 / 4224 layout (r01 v7: 65 % conflict cycles)
-  static constexpr int XP = 88;
-  static constexpr int XPL = 1072;                 // >= XROWS * XP = 1056
-  static constexpr int XCP = 4292;                 // >= C * XPL = 4288
+  // Row / channel-plane / copy pitches (16-bit units) and the tap order of the A rows, from the
+  // bank model of the A-fragment dword reads (2 x 32-lane groups, bank = dword mod 32).  A
+  // 32-lane group reads 4 taps x 4 channels x 2 pixel runs; channel planes add multiples of 8
+  // dwords (XPL / 2 = 552 = 8 mod 32), pixel runs 4, so the reads are conflict-free when the 4
+  // taps of an m-tile have distinct tap offsets mod 4 dwords.  With XP / 2 = 45 (1 mod 4) and
+  // XCP / 2 = 2210 (2 mod 4) the 25 taps fall 6 / 6 / 7 / 6 into the residues and C0W_TAP puts
+  // one of each into every m-tile (padding slots read a tap of the missing residue): 1.00 LDS
+  // cycles per read (r02: 1.43 with 88 / 1072 / 4292 and taps in order; r01: 3.71 dense)
+  static constexpr int XP = 90;
+  static constexpr int XPL = 1104;                 // >= XROWS * XP = 1080
+  static constexpr int XCP = 4420;                 // >= C * XPL = 4416
   static constexpr int X_16 = 2 * XCP;
   static constexpr int LDS_U4 = ((Y_16 + X_16) * 2 + YC_BYTES) / 16;
   static constexpr int MT = 7, M = NTAP * C;
@@ -441,6 +455,8 @@ struct Conv0W {
   static_assert(KSTEPS % 4 == 0 && COUT * PRB * (PW / 4) % 256 == 0 && NXV <= 256, "geom");
   static_assert(HO % RB == 0 && RB + KT - 1 + HO - RB <= HS, "band rows stay inside the frame");
   static_assert(WO % 8 == 0 && ((Y_16 + X_16) * 2) % 16 == 0, "layout");
+  static_assert(XPL >= XROWS * XP && XCP >= C * XPL && XP % 2 == 0 && XPL % 2 == 0 && XCP % 2 == 0,
+                "X planes: disjoint, dword-aligned pixel pairs");
 };
 
 struct Conv0WArgs {
@@ -512,8 +528,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
         uint32_t b[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j] = u8pair<NS>((px[j] >> (8 * c)) & 255u, 0u) & 0xFFFFu;
-        uint16_t* p0 = xs + c * G::XPL + r * G::XP + x;              // copy 0
-        *reinterpret_cast<uint2*>(p0) = make_uint2(b[0] | (b[1] << 16), b[2] | (b[3] << 16));
+        uint16_t* p0 = xs + c * G::XPL + r * G::XP + x;              // copy 0 (4-byte aligned:
+        reinterpret_cast<uint32_t*>(p0)[0] = b[0] | (b[1] << 16);       // odd rows sit at 4 mod 8)
+        reinterpret_cast<uint32_t*>(p0)[1] = b[2] | (b[3] << 16);
         uint16_t* p1 = xs + G::XCP + c * G::XPL + r * G::XP + x;     // copy 1: column x - 1
         if (x > 0) p1[-1] = (uint16_t)b[0];
         *reinterpret_cast<uint32_t*>(p1) = b[1] | (b[2] << 16);
@@ -526,8 +543,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
   int aoff[G::MT];
 #pragma unroll
   for (int mt = 0; mt < G::MT; ++mt) {
-    int tap = 4 * mt + (li >> 2);
-    if (tap >= G::NTAP) tap = 0;                       // padded rows: discarded
+    const int tap = C0W_TAP_ADDR[4 * mt + (li >> 2)];   // padding slots: discarded rows
     const int c = li & 3, kh = tap / G::KT, kw = tap % G::KT, h = kw & 1;
     aoff[mt] = h * G::XCP + c * G::XPL + kh * G::XP + (kw - h);
   }
@@ -599,8 +615,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = 16 * mt + 4 * lq + r;
-        if (m < G::M) red[(wave * G::M + m) * G::COUT + 16 * nt + li] = acc[mt][nt][r];
+        const int tap = C0W_TAP_OUT[4 * mt + lq];        // row 4 lq + r = (slot lq, channel r)
+        if (tap >= 0) red[(wave * G::M + tap * G::C + r) * G::COUT + 16 * nt + li] = acc[mt][nt][r];
       }
   __syncthreads();
   float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
