@@ -145,19 +145,31 @@ class Ba3cEngine(object):
                                          _ptr(out[0]), _ptr(out[1]), _ptr(out[2])))
         return out
 
-    def train_grads(self, state, action, futurereward, entropy_beta=0.01, grads=None):
+    def train_grads(self, state, action, futurereward, entropy_beta=0.01, grads=None, phase=0):
         """Forward + loss + backward; raw gradients into `grads` (default self.grads).
-        Returns the device float64 scalars tensor (order: _lib.SCALAR_NAMES)."""
+        Returns the device float64 scalars tensor (order: _lib.SCALAR_NAMES).  phase 1 / 2
+        split the pass at the fc1 + heads bucket (ba3c_train_grads_phase)."""
         B = self._check_state(state)
         assert action.dtype == torch.int64 and action.shape == (B,) and action.is_cuda
         assert futurereward.dtype == torch.float32 and futurereward.shape == (B,)
         grads = self.grads if grads is None else grads
-        _lib.check(self.lib.ba3c_train_grads(self.h, _stream(), _ptr(self.params), _ptr(state),
-                                             _ptr(action.contiguous()),
-                                             _ptr(futurereward.contiguous()), B,
-                                             float(entropy_beta), _ptr(self._workspace(True)),
-                                             _ptr(grads), _ptr(self.scalars)))
+        _lib.check(self.lib.ba3c_train_grads_phase(self.h, _stream(), _ptr(self.params), _ptr(state),
+                                                   _ptr(action.contiguous()),
+                                                   _ptr(futurereward.contiguous()), B,
+                                                   float(entropy_beta), _ptr(self._workspace(True)),
+                                                   _ptr(grads), _ptr(self.scalars), int(phase)))
         return self.scalars
+
+    def bucket_split(self):
+        """(first tensor, flat offset) of the fc1 + heads gradient bucket."""
+        t = int(self.lib.ba3c_bucket_tensor(self.h))
+        return t, self.layout[t][1]
+
+    def clip_grads_range(self, t0, t1, grads=None):
+        """clip_by_average_norm over tensors [t0, t1) only."""
+        grads = self.grads if grads is None else grads
+        _lib.check(self.lib.ba3c_clip_grads_range(self.h, _stream(), _ptr(grads),
+                                                  _ptr(self._workspace(True)), int(t0), int(t1)))
 
     def clip_grads(self, grads=None):
         """tf.clip_by_average_norm(g, 0.1) per tensor, in place (train.py:329-330)."""

@@ -60,7 +60,10 @@ class Model(ModelDesc):
                 state, explore_factor=self.explore_factor)
             return
         self.delay = inputs[3] if len(inputs) > 3 else None
-        sc = self.engine.train_grads(state, action, futurereward, entropy_beta=self.entropy_beta)
+        # train_phase 1 / 2: the two halves of the pass around the fc1 + heads gradient bucket
+        # (Ba3cTrainer's bucketed data-parallel step); 0: the whole pass
+        sc = self.engine.train_grads(state, action, futurereward, entropy_beta=self.entropy_beta,
+                                     phase=getattr(self, "train_phase", 0))
         self.scalars = sc
         self.cost = sc[0]
 

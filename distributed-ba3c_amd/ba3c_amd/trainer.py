@@ -51,8 +51,12 @@ class Ba3cTrainer(object):
 
     def train_step(self, state, action, futurereward):
         """Device-side step with no host synchronisation (used by bench.py)."""
-        self.model.build_graph([state, action, futurereward])
         opt = self.optimizer
+        if isinstance(opt, SyncReplicasOptimizer) and self._fused_clip and opt.bucketed:
+            self._bucketed_sync_step(state, action, futurereward)
+            self.global_step += 1
+            return
+        self.model.build_graph([state, action, futurereward])
         if isinstance(opt, SyncReplicasOptimizer):
             if self._fused_clip:
                 opt.aggregate(self.engine)
@@ -66,6 +70,29 @@ class Ba3cTrainer(object):
             self.process_grads()
             opt.apply_gradients(self.engine)
         self.global_step += 1
+
+    def _bucketed_sync_step(self, state, action, futurereward):
+        """Data-parallel step with the gradient exchange in two buckets: phase 1 of the pass
+        (forward, loss, heads + fc1 backward) -> clip + async RCCL sum of the fc1 + heads
+        bucket -> phase 2 (conv backward, overlapping that all-reduce) -> clip + RCCL sum of
+        the conv bucket -> wait -> the identical update on every rank (grad_scale = 1/N)."""
+        eng, opt, m = self.engine, self.optimizer, self.model
+        tb, off = eng.bucket_split()
+        nt, total = len(eng.layout), eng.grads.numel()
+        inputs = [state, action, futurereward]
+        m.train_phase = 1
+        try:
+            m.build_graph(inputs)
+            work = opt.aggregate_bucket_async(eng, tb, nt, off, total)
+            m.train_phase = 2
+            m.build_graph(inputs)
+        finally:
+            m.train_phase = 0
+        work2 = opt.aggregate_bucket_async(eng, 0, tb, 0, off)
+        for w in (work, work2):
+            if w is not None:
+                w.wait()
+        opt.apply_gradients(eng)
 
     def capture_step(self, state, action, futurereward, warmup=2):
         """Capture one full step (fwd+bwd+clip+update) on static input tensors as a hipGraph

@@ -360,7 +360,6 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
         constexpr int N16 = HALO * L::RP / 16;
         const uint4* src = reinterpret_cast<const uint4*>(lds + G::RB * L::RP);
         uint4* dst = reinterpret_cast<uint4*>(lds);
-#pragma unroll
         for (int i = tid; i < N16; i += 256) dst[i] = src[i];
         fbase = (unsigned)HALO * G::WS * O::Q;              // stage rows HALO .. SROWS-1 only
       }

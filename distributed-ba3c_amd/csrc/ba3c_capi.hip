@@ -449,7 +449,9 @@ int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, cons
   {
     ProbeScope ps(h, s, kid);
     if constexpr (L::NPH == 1 && L::G::NBANDS > 1 && L::G::SROWS > L::G::RB) {
-      if (pipelined && h->ring && a.batch >= 2 * h->cus) {
+      // whole images per workgroup: only where they split (nearly) evenly over 2 x CUs
+      const int pr = 2 * h->cus;
+      if (pipelined && h->ring && a.batch >= pr && (a.batch % pr == 0 || a.batch >= 8 * pr)) {
         hipLaunchKernelGGL(conv_band6r_kernel<L>, dim3(2 * h->cus), dim3(256), 0, s, b);
         HIP_TRY(hipGetLastError());
         return BA3C_OK;
@@ -741,9 +743,13 @@ int ensure_side_stream(ba3c_handle* h, hipStream_t s) {
   return BA3C_OK;
 }
 
+// phase 0: the whole backward pass.  phase 1: the heads and fc1 products and their
+// reductions (those gradients are final when it returns); phase 2: conv3..conv0 and theirs.
+// Phases 1 + 2 compute exactly phase 0; between them a data-parallel caller can all-reduce
+// the fc1 + heads bucket (most of the parameters) while the conv layers run.
 template <int CH, int NS>
 int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
-                 const Workspace& w, float* grads) {
+                 const Workspace& w, float* grads, int phase = 0) {
   using LY = Lay<NS>;
   const int F = h->cfg.fc_neurons, A = h->cfg.num_actions;
   const bool legacy = !h->cfg.replace_with_conv;
@@ -785,8 +791,23 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
     ~DeferGuard() { h->defer_reduce = false; }
   } defer_guard(h);
+  // join the side stream and run the deferred reductions of this phase in one launch
+  auto finish = [&]() -> int {
+    if (ws != s) {
+      HIP_TRY(hipEventRecord(h->ev_join, ws));
+      HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
+    }
+    const ReduceJobs& jb = h->rjobs;
+    if (jb.n > 0) {
+      ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
+      hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(256), 0, s, jb);
+    }
+    HIP_TRY(hipGetLastError());
+    return BA3C_OK;
+  };
   CHECK(fork());
 
+  if (phase != 2) {
   // heads: d fc-pi/W, fc-pi/b, fc-v/W, fc-v/b  (X = h, G = [dz | dV])
   {
     WgradPlan pl = plan_wgrad(F + 1, A + 1, B, 128, 32);
@@ -835,6 +856,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     if (!mj_fc) CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_FC1_DGRAD, d, 1)));
     CHECK(fork());
   }
+  }  // phase != 2
+  if (phase == 1) return finish();
   auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad, const float* part) {
     ReduceMap mp{};
     mp.kind = 0;
@@ -976,18 +999,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.dst = grads + h->tensors[h->idx_conv[0]].offset;
     CHECK(launch_reduce(h, s, w.part0, pl.S, mp));
   }
-  if (ws != s) {
-    HIP_TRY(hipEventRecord(h->ev_join, ws));
-    HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
-  }
-  // all weight-gradient reductions: one launch, every gradient element written once
-  {
-    const ReduceJobs& jb = h->rjobs;
-    ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
-    hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(256), 0, s, jb);
-  }
-  HIP_TRY(hipGetLastError());
-  return BA3C_OK;
+  // all (remaining) weight-gradient reductions: one launch, every gradient element written once
+  return finish();
 }
 
 int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, int B,
@@ -1235,9 +1248,33 @@ int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_
                    probsT, value);
 }
 
+static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                            const int64_t* action, const float* futurereward, int32_t batch,
+                            float entropy_beta, void* workspace, float* grads, double* scalars,
+                            int32_t phase);
+
 int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                      const int64_t* action, const float* futurereward, int32_t batch,
                      float entropy_beta, void* workspace, float* grads, double* scalars) {
+  return train_grads_impl(h, stream, params, state, action, futurereward, batch, entropy_beta, workspace,
+                          grads, scalars, 0);
+}
+
+int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                           const int64_t* action, const float* futurereward, int32_t batch,
+                           float entropy_beta, void* workspace, float* grads, double* scalars,
+                           int32_t phase) {
+  if (phase < 0 || phase > 2) return fail(BA3C_ERR_INVALID, "phase must be 0, 1 or 2");
+  return train_grads_impl(h, stream, params, state, action, futurereward, batch, entropy_beta, workspace,
+                          grads, scalars, phase);
+}
+
+int ba3c_bucket_tensor(const ba3c_handle* h) { return h ? h->idx_fc1 : -1; }
+
+static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                            const int64_t* action, const float* futurereward, int32_t batch,
+                            float entropy_beta, void* workspace, float* grads, double* scalars,
+                            int32_t phase) {
   if (!h || !check_ptr(params) || !check_ptr(state) || !check_ptr(workspace) || !check_ptr(grads) ||
       !action || !futurereward)
     return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
@@ -1247,6 +1284,11 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
   Workspace w = carve(h, workspace, batch, true);
   // no memset of `grads`: the backward pass's single reduction launch writes every element
   // of every tensor (incl. conv0's zero-padded channels)
+  if (phase == 2)   // conv layers' backward on the workspace phase 1 left
+    return h->cfg.channels == 4 ? (h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads, 2)
+                                              : run_backward<4, 3>(h, s, params, state, batch, w, grads, 2))
+                                : (h->ns == 2 ? run_backward<12, 2>(h, s, params, state, batch, w, grads, 2)
+                                              : run_backward<12, 3>(h, s, params, state, batch, w, grads, 2));
   // on the band + split path the weight-prep launch zeroes the ReLU counters
   if (!(h->band && h->b6)) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_WORDS * 8, s));
   int r = h->cfg.channels == 4 ? (h->ns == 2 ? run_forward<4, 2>(h, s, params, state, batch, w, true)
@@ -1258,10 +1300,23 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
   CHECK(run_heads(h, s, params, w, batch, action, futurereward, entropy_beta, 1.0f, true, nullptr,
                   nullptr, nullptr, scalars));
   if (h->cfg.channels == 4)
-    return h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads)
-                      : run_backward<4, 3>(h, s, params, state, batch, w, grads);
-  return h->ns == 2 ? run_backward<12, 2>(h, s, params, state, batch, w, grads)
-                    : run_backward<12, 3>(h, s, params, state, batch, w, grads);
+    return h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads, phase)
+                      : run_backward<4, 3>(h, s, params, state, batch, w, grads, phase);
+  return h->ns == 2 ? run_backward<12, 2>(h, s, params, state, batch, w, grads, phase)
+                    : run_backward<12, 3>(h, s, params, state, batch, w, grads, phase);
+}
+
+int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* workspace, int32_t t0,
+                          int32_t t1) {
+  if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
+  if (t0 < 0 || t1 > h->table.n || t0 >= t1) return fail(BA3C_ERR_INVALID, "bad tensor range");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* part = carve(h, workspace, 1, false).sumsq;
+  const int c0 = h->table.chunk0[t0], nc = h->table.chunk0[t1] - c0;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, part, c0);
+  hipLaunchKernelGGL(clip_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, (const float*)part, c0);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
 }
 
 int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace) {
@@ -1270,9 +1325,9 @@ int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace)
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
   {
     ProbeScope ps(h, s, BA3C_K_CLIP);
-    hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part);
+    hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part, 0);
     hipLaunchKernelGGL(clip_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table,
-                       (const float*)part);
+                       (const float*)part, 0);
   }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
@@ -1328,7 +1383,7 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
     return BA3C_OK;   // the Adam device powers advanced inside the launch
   }
   if (fuse_clip) {
-    hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part);
+    hipLaunchKernelGGL(sumsq_kernel, dim3(h->table.nchunks), dim3(256), 0, s, grads, h->table, part, 0);
     HIP_TRY(hipGetLastError());
     a.clip_part = part;
   }

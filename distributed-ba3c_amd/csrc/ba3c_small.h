@@ -478,10 +478,11 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
   return r;
 }
 
+// cbase: first chunk of the launch (a tensor-aligned range of the table)
 __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g, const TensorTable tt,
-                                                    float* __restrict__ part) {
+                                                    float* __restrict__ part, int cbase) {
   __shared__ float red[4];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x + cbase;
   const int t = table_find(tt, b);
   const int c = b - tt.chunk0[t];
   const int beg = c * UPD_CHUNK;
@@ -505,8 +506,8 @@ __device__ __forceinline__ float clip_factor(const TensorTable& tt, int t, const
 }
 
 __global__ void __launch_bounds__(256) clip_kernel(float* __restrict__ g, const TensorTable tt,
-                                                   const float* __restrict__ part) {
-  const int b = blockIdx.x;
+                                                   const float* __restrict__ part, int cbase) {
+  const int b = blockIdx.x + cbase;
   const int t = table_find(tt, b);
   const int c = b - tt.chunk0[t];
   const int beg = c * UPD_CHUNK;

@@ -110,9 +110,10 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
   uint32_t yc[YPT];                                       // (un-loaded: dY is zero)
 
   const int nbands = a.batch * G::NBANDS;
-  // band walk: whole images per workgroup (ring reuse of the halo rows) when every workgroup
-  // gets at least one image, else bands bx, bx + gx, ... (small batches)
-  const bool ring = G::RING && a.batch >= gx;
+  // band walk: whole images per workgroup (ring reuse of the halo rows) when the images split
+  // evenly over the workgroups (or nearly: >= 8 each), else bands bx, bx + gx, ... (balanced
+  // at any batch)
+  const bool ring = G::RING && a.batch >= gx && (a.batch % gx == 0 || a.batch >= 8 * gx);
   int band_end = nbands;
   int band = bx;
   if (ring) {

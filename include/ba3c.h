@@ -142,8 +142,25 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
                      const int64_t* action, const float* futurereward, int32_t batch,
                      float entropy_beta, void* workspace, float* grads, double* scalars);
 
+/* ba3c_train_grads in two phases for data-parallel bucketing: phase 1 runs the
+ * forward, the loss / scalars and the backward of the heads and fc1 and leaves THEIR gradient
+ * tensors (tensors ba3c_bucket_tensor(h) .. end of the flat layout) final; phase 2 (same
+ * arguments, same workspace) runs conv3..conv0 and finishes the rest.  Phase 0 = both = the
+ * bit-identical ba3c_train_grads.  Between the phases the caller may clip and all-reduce the
+ * fc1 + heads bucket while the conv layers run (the reference's per-variable PS pushes,
+ * OpenAIGym/train.py:598-606). */
+int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
+                           const int64_t* action, const float* futurereward, int32_t batch,
+                           float entropy_beta, void* workspace, float* grads, double* scalars,
+                           int32_t phase);
+/* First tensor of the fc1 + heads bucket (tensors before it: the conv layers). */
+int ba3c_bucket_tensor(const ba3c_handle* h);
+
 /* Per-tensor tf.clip_by_average_norm(g, 0.1) in place (n = graph numel incl. padding). */
 int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace);
+/* The same clip over tensors [t0, t1) only (a bucket). */
+int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* workspace, int32_t t0,
+                          int32_t t1);
 
 /* One optimizer apply over the flat buffers: g_eff = grads*grad_scale (1/world after an
  * all-reduce-sum), or, with fuse_clip=1, clip_by_average_norm(grads) fused in (single

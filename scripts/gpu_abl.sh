@@ -17,4 +17,4 @@ done
 for f in gpurun_out/$tag/*.log; do grep -h '^{' $f | python -c "
 import sys,json
 d=json.loads(sys.stdin.read()); k=d['kernel_ms_one_step']
-print('$f'.split('/')[-1], d['value'], d['ms_per_step'], d['ms_per_step_median'], json.dumps({x: k[x] for x in ('conv0_fwd','conv1_fwd','conv1_dgrad','conv2_fwd','conv2_dgrad','conv1_wgrad')}))"; done
+print('$f'.split('/')[-1], d['value'], d['ms_per_step'], d['ms_per_step_median'], json.dumps({x: k[x] for x in ('conv0_fwd','conv1_fwd','conv1_dgrad','conv2_dgrad','conv1_wgrad','heads','fc1_fwd')}))"; done

@@ -155,3 +155,31 @@ def test_ring_walk_band_kernels_match_one_band_kernels(monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
     for n in out[0][2]:
         assert torch.equal(out[0][2][n], out[1][2][n]), n
+
+
+@pytest.mark.parametrize("B", [32, 160])
+def test_two_phase_backward_equals_one_pass(B):
+    """ba3c_train_grads_phase 1 then 2 (the bucketed data-parallel step splits the pass at the
+    fc1 + heads bucket) gives the one-pass gradients and scalars bit for bit; after phase 1 the
+    bucket's tensors are already final."""
+    from ba3c_amd.engine import Ba3cEngine
+    rs = np.random.RandomState(79)
+    state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    eng = Ba3cEngine(num_actions=4, fc_neurons=128, fc_splits=4, max_batch=B)
+    eng.load_params(O.init_params(128, 4, 4, seed=9, dtype=np.float32))
+    sc = eng.train_grads(state, action, R).clone()
+    ref = eng.grads.clone()
+    eng.grads.fill_(0.5)                       # every tensor element must be rewritten
+    eng.train_grads(state, action, R, phase=1)
+    t, off = eng.bucket_split()
+    assert eng.layout[t][0].startswith("fc1")
+    mid = eng.grads.clone()
+    sc1 = eng.train_grads(state, action, R, phase=2)
+    torch.cuda.synchronize()
+    for i, (name, o, n, _) in enumerate(eng.layout):   # (the 64-float alignment gaps are not
+        if i >= t:                                      # gradient elements)
+            assert torch.equal(mid[o:o + n], ref[o:o + n]), name
+        assert torch.equal(eng.grads[o:o + n], ref[o:o + n]), name
+    assert torch.equal(sc1, sc)

@@ -39,6 +39,14 @@ class OracleEngine(object):
     def tensor_names(self):
         return self.names
 
+    @property
+    def layout(self):
+        return [(k, self.offs[k], int(np.prod(self.shapes[k])), self.shapes[k]) for k in self.names]
+
+    def bucket_split(self):
+        t = next(i for i, k in enumerate(self.names) if k.startswith("fc"))
+        return t, self.offs[self.names[t]]
+
     def state_dict(self, flat=None):
         flat = (self.params if flat is None else flat).numpy()
         return {k: flat[self.offs[k]:self.offs[k] + int(np.prod(self.shapes[k]))].reshape(self.shapes[k]).copy()
@@ -47,16 +55,31 @@ class OracleEngine(object):
     def zeros_like_flat(self, fill=0.0):
         return torch.full((self.flat_size,), fill, dtype=torch.float32)
 
-    def train_grads(self, state, action, R, entropy_beta=0.01, grads=None):
-        _, sc, g = O.loss_and_grads(self.state_dict(), state.numpy(), action.numpy(), R.numpy(), CFG)
-        self.grads.copy_(torch.from_numpy(np.concatenate([g[k].reshape(-1) for k in self.names])))
-        self.scalars[0] = float(sc["cost"])
+    def train_grads(self, state, action, R, entropy_beta=0.01, grads=None, phase=0):
+        # phase 1 leaves the fc1 + heads bucket final, phase 2 the conv part (the HIP engine's
+        # contract: each phase writes only its own bucket)
+        _, off = self.bucket_split()
+        if phase != 2:
+            _, sc, g = O.loss_and_grads(self.state_dict(), state.numpy(), action.numpy(), R.numpy(), CFG)
+            self._full = torch.from_numpy(np.concatenate([g[k].reshape(-1) for k in self.names]))
+            self.scalars[0] = float(sc["cost"])
+        if phase == 0:
+            self.grads.copy_(self._full)
+        elif phase == 1:
+            self.grads[off:].copy_(self._full[off:])
+        else:
+            self.grads[:off].copy_(self._full[:off])
         return self.scalars
 
     def clip_grads(self, grads=None):
+        self.clip_grads_range(0, len(self.names))
+
+    def clip_grads_range(self, t0, t1, grads=None):
         g = self.state_dict(self.grads)
-        self.grads.copy_(torch.from_numpy(np.concatenate(
-            [O.clip_by_average_norm(g[k]).reshape(-1) for k in self.names])))
+        for k in self.names[t0:t1]:
+            n = int(np.prod(self.shapes[k]))
+            self.grads[self.offs[k]:self.offs[k] + n].copy_(
+                torch.from_numpy(O.clip_by_average_norm(g[k]).reshape(-1)))
 
     def apply_update(self, opt, slot0, slot1, hp, grad_scale=1.0, fuse_clip=False, grads=None,
                      dev_powers=None):
@@ -80,7 +103,7 @@ def _batch(seed, B=2):
             rs.randint(0, 4, size=B).astype(np.int64), rs.normal(size=B).astype(np.float32))
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, bucketed=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -91,6 +114,7 @@ def _worker(rank, world, port, out):
     eng = OracleEngine(params)
     model = Model(num_actions=4, fc_neurons=16, fc_splits=2, batch_size=2, engine=eng)
     opt = SyncReplicasOptimizer(AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), world, world)
+    opt.bucketed = bucketed
     tr = Ba3cTrainer(TrainConfig(model=model, optimizer=opt))
     for step in range(2):
         s, a, r = _batch(10 * step + rank)
@@ -107,11 +131,14 @@ def _free_port():
     return p
 
 
-def test_sync_replicas_world2_gloo_matches_oracle_sync_step():
+@pytest.mark.parametrize("bucketed", [True, False])
+def test_sync_replicas_world2_gloo_matches_oracle_sync_step(bucketed):
+    """Both exchanges — two buckets (fc1 + heads all-reduced beside the conv backward) and one
+    flat all-reduce — equal the oracle's SyncReplicas step."""
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, bucketed), nprocs=world, join=True)
     # replicas stay bit-identical
     np.testing.assert_array_equal(out[0], out[1])
     # and equal the oracle's SyncReplicas step: mean of per-replica clipped grads, one Adam
