@@ -345,6 +345,16 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
   const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
   const int ipw = (a.batch + gx - 1) / gx;
   const int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
+  // PRE (input-gradient layouts, whose registers allow it): the next band's RB new rows are
+  // loaded into registers before this band's MFMAs, so their global latency hides behind them
+#ifndef BA3C_RING_PRE
+#define BA3C_RING_PRE 1
+#endif
+  constexpr bool PRE = BA3C_RING_PRE && G::SRC == 1;
+  constexpr unsigned FNEW = (unsigned)HALO * G::WS * O::Q;  // first float4 index of the new rows
+  constexpr int NNEW = (G::RB * G::WS * O::Q + 255) / 256;
+  float4 pv[PRE ? NNEW : 1];
+  uint32_t pc[PRE ? NNEW : 1];
   unsigned long long pos = 0;
   for (int img = img0; img < img1; ++img) {
     const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
@@ -361,20 +371,31 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
         const uint4* src = reinterpret_cast<const uint4*>(lds + G::RB * L::RP);
         uint4* dst = reinterpret_cast<uint4*>(lds);
         for (int i = tid; i < N16; i += 256) dst[i] = src[i];
-        fbase = (unsigned)HALO * G::WS * O::Q;              // stage rows HALO .. SROWS-1 only
+        fbase = FNEW;                                       // stage rows HALO .. SROWS-1 only
       }
-      // staging of rows [fbase / (WS Q), rows_out + KH - 1), loads in chunks, then the stores
-      const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * O::Q;
-      constexpr int NPT = O::NTOT < BA3C_STAGE_NPT ? O::NTOT : BA3C_STAGE_NPT;
-      for (unsigned base = fbase; base < nvec; base += 256u * NPT) {
-        float4 v[NPT];
-        uint32_t cd[NPT];
+      if (PRE && bi > 0) {
+        // the new rows were prefetched during the previous band's MFMAs
 #pragma unroll
-        for (int i = 0; i < NPT; ++i) O::load1(a, img, y0, rows_out, 0, base + tid + 256u * i, v[i], cd[i]);
+        for (int i = 0; i < NNEW; ++i) O::store1(lds, y0, rows_out, FNEW + tid + 256u * i, pv[i], pc[i], asc);
+      } else {
+        // staging of rows [fbase / (WS Q), rows_out + KH - 1), loads in chunks, then the stores
+        const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * O::Q;
+        constexpr int NPT = O::NTOT < BA3C_STAGE_NPT ? O::NTOT : BA3C_STAGE_NPT;
+        for (unsigned base = fbase; base < nvec; base += 256u * NPT) {
+          float4 v[NPT];
+          uint32_t cd[NPT];
 #pragma unroll
-        for (int i = 0; i < NPT; ++i) O::store1(lds, y0, rows_out, base + tid + 256u * i, v[i], cd[i], asc);
+          for (int i = 0; i < NPT; ++i) O::load1(a, img, y0, rows_out, 0, base + tid + 256u * i, v[i], cd[i]);
+#pragma unroll
+          for (int i = 0; i < NPT; ++i) O::store1(lds, y0, rows_out, base + tid + 256u * i, v[i], cd[i], asc);
+        }
       }
       __syncthreads();
+      if (PRE && bi + 1 < G::NBANDS) {
+        const int y1 = y0 + G::RB, ro1 = min(G::RB, G::HO - y1);
+#pragma unroll
+        for (int i = 0; i < NNEW; ++i) O::load1(a, img, y1, ro1, 0, FNEW + tid + 256u * i, pv[i], pc[i]);
+      }
       O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [](int) {});
     }
     if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
