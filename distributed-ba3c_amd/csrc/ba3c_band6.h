@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
 // band's staging VALU and global reads drop by (KH - 1) / SROWS (40 % for conv1 fwd's 6-row
 // bands, 50 % for conv1 dgrad's 4-row ones).  Per band the LDS image and the MFMA stream are
 // the one-band kernel's, so the outputs are bit-identical.
-template <class L>
+template <class L, bool PRE_ = L::G::SRC == 1>
 __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, char* lds) {
   static_assert(L::NPH == 1 && L::G::SROWS > L::G::RB, "ring walk: unphased layouts with a halo");
   using O = Band6Ops<L>;
@@ -350,7 +350,7 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
 #ifndef BA3C_RING_PRE
 #define BA3C_RING_PRE 1
 #endif
-  constexpr bool PRE = BA3C_RING_PRE && G::SRC == 1;
+  constexpr bool PRE = BA3C_RING_PRE && PRE_;
   constexpr unsigned FNEW = (unsigned)HALO * G::WS * O::Q;  // first float4 index of the new rows
   constexpr int NNEW = (G::RB * G::WS * O::Q + 255) / 256;
   float4 pv[PRE ? NNEW : 1];
@@ -403,10 +403,10 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
   if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
 
-template <class L>
+template <class L, bool PRE_ = L::G::SRC == 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6r_kernel(const Band6Args a) {
   __shared__ uint4 lds4[L::LDS_BYTES / 16];
-  band6r_body<L>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
+  band6r_body<L, PRE_>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
 }
 
 // Pipelined persistent variant (NPH == 1 layouts): one 512-thread workgroup per CU walks
