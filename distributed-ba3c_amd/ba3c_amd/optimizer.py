@@ -171,6 +171,19 @@ def make_optimizer(name, lr, beta1=0.9, beta2=0.999, epsilon=1e-8):
     raise ValueError("unknown optimizer %r" % name)
 
 
+class _StagedWork(object):
+    """Work handle of a host-staged all-reduce: wait() completes it and copies the sum back
+    into the device buffer (on the current stream, so later kernels see it)."""
+
+    def __init__(self, work, host, dst):
+        self.work, self.host, self.dst = work, host, dst
+
+    def wait(self):
+        self.work.wait()
+        self.dst.copy_(self.host)
+        return True
+
+
 class SyncReplicasOptimizer(object):
     """tf.train.SyncReplicasOptimizer(opt, replicas_to_aggregate, total_num_replicas)
     (train.py:598-606) on one node: every rank clips its own gradients, the flat buffer is
@@ -212,17 +225,37 @@ class SyncReplicasOptimizer(object):
         restore), as all workers of the reference read the one PS copy (train.py:512-515)."""
         if not self.distributed:
             return
-        dist.broadcast(engine.params, src=src, group=self.group)
-        for t in (self._opt.slots or []):
-            dist.broadcast(t, src=src, group=self.group)
-        if self._opt.dev_powers is not None:
-            dist.broadcast(self._opt.dev_powers, src=src, group=self.group)
+        for t in [engine.params] + list(self._opt.slots or []) + (
+                [self._opt.dev_powers] if self._opt.dev_powers is not None else []):
+            if self._staged(t):
+                host = t.cpu()
+                dist.broadcast(host, src=src, group=self.group)
+                t.copy_(host)
+            else:
+                dist.broadcast(t, src=src, group=self.group)
+
+    def _staged(self, t):
+        """gloo group + device tensor (several replicas sharing one GPU, where RCCL refuses
+        two ranks on one device; tests and CPU rehearsals): the exchange goes through a host
+        copy.  RCCL ('nccl') takes the device buffer directly."""
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
+    def _all_reduce(self, t, async_op=False):
+        if not self._staged(t):
+            return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+        host = t.cpu()                     # waits for the producing kernels on this stream
+        work = dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        staged = _StagedWork(work, host, t)
+        if async_op:
+            return staged
+        staged.wait()
+        return None
 
     def allreduce(self, engine):
         """Sum of the replicas' flat gradient buffers over RCCL ('nccl' backend), issued on the
         current HIP stream; runs whenever a process group exists (also at world size 1)."""
         if self.distributed:
-            dist.all_reduce(engine.grads, op=dist.ReduceOp.SUM, group=self.group)
+            self._all_reduce(engine.grads)
 
     def aggregate(self, engine):
         """Per-replica clip (multigpu.py:157) then the RCCL sum of the clipped buffer."""
@@ -240,8 +273,7 @@ class SyncReplicasOptimizer(object):
         engine.clip_grads_range(t0, t1)
         if not self.distributed:
             return None
-        return dist.all_reduce(engine.grads[off0:off1], op=dist.ReduceOp.SUM, group=self.group,
-                               async_op=True)
+        return self._all_reduce(engine.grads[off0:off1], async_op=True)
 
     def apply_gradients(self, engine):
         self._opt.apply_gradients(engine, grad_scale=1.0 / self.world, fuse_clip=False)

@@ -110,6 +110,7 @@ class _Metrics(object):
             return
         from ._lib import SCALAR_NAMES
         vals = torch.stack(self.pending).cpu().numpy()
+        self.trainer.check_device_errors()           # the host has synchronised anyway
         dt = time.time() - self.t0
         dp_per_s = len(self.pending) * self.B / max(dt, 1e-9)      # multigpu.py:307-313
         for row in vals:

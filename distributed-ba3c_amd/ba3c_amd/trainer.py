@@ -49,6 +49,17 @@ class Ba3cTrainer(object):
         for p in self._procs:
             p.process(self.engine)
 
+    def check_device_errors(self):
+        """Abort on an in-launch wait that gave up (ba3c_device_errors != 0): the fused
+        clip + update kernel then applied a clip factor from stale partials, so the parameters
+        are no longer the reference's.  Called where the host already synchronises (run_step,
+        the metrics flush of train.py); it synchronises the device itself."""
+        f = self.engine.device_errors() if hasattr(self.engine, "device_errors") else 0
+        if f:
+            raise RuntimeError("device error flags 0x%x after global step %d: an in-launch "
+                               "grid wait gave up (fused clip + update); rerun with "
+                               "BA3C_FUSED_UPDATE=0" % (f, self.global_step))
+
     def train_step(self, state, action, futurereward):
         """Device-side step with no host synchronisation (used by bench.py)."""
         opt = self.optimizer
@@ -141,6 +152,7 @@ class Ba3cTrainer(object):
         R = torch.as_tensor(np.asarray(batch[2], dtype=np.float32)).to(dev)
         self.train_step(state, action, R)
         out = self.model.scalars_dict()      # synchronises the stream
+        self.check_device_errors()
         if len(batch) > 3 and batch[3] is not None:
             out["delay"] = float(np.mean(self.global_step - np.asarray(batch[3], np.float64)))
         out["global_step"] = self.global_step

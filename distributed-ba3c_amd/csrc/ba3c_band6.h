@@ -334,7 +334,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
 // KH-2, disjoint ranges) and only the RB new rows are loaded, un-pooled and split — the
 // band's staging VALU and global reads drop by (KH - 1) / SROWS (40 % for conv1 fwd's 6-row
 // bands, 50 % for conv1 dgrad's 4-row ones).  Per band the LDS image and the MFMA stream are
-// the one-band kernel's, so the outputs are bit-identical.
+// the one-band kernel's, so the outputs are bit-identical.  (Round 2 ran the copy and the new-row
+// stores with no barrier in between: a cross-wave write-after-read race in LDS; fixed in r03.)
 template <class L, bool PRE_ = L::G::SRC == 1>
 __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, char* lds) {
   static_assert(L::NPH == 1 && L::G::SROWS > L::G::RB, "ring walk: unphased layouts with a halo");
@@ -366,12 +367,17 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
       __syncthreads();                                      // previous band's LDS reads are done
       unsigned fbase = 0;
       if (bi > 0) {
-        // carry the halo rows down (disjoint source / destination rows)
+        // carry the halo rows down: source rows RB .. SROWS-1 -> rows 0 .. HALO-1.  The new
+        // rows then go to rows HALO .. SROWS-1, which overlap the source rows (RB >= HALO), and
+        // a thread's copy elements are not the rows its stores write: every wave's copy must
+        // be complete before any wave stores (the barrier below; without it a fast wave could
+        // overwrite halo bytes a slower wave has not copied yet)
         constexpr int N16 = HALO * L::RP / 16;
         const uint4* src = reinterpret_cast<const uint4*>(lds + G::RB * L::RP);
         uint4* dst = reinterpret_cast<uint4*>(lds);
         for (int i = tid; i < N16; i += 256) dst[i] = src[i];
         fbase = FNEW;                                       // stage rows HALO .. SROWS-1 only
+        __syncthreads();
       }
       if (PRE && bi > 0) {
         // the new rows were prefetched during the previous band's MFMAs

@@ -240,8 +240,14 @@ __global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B,
 }
 
 // One wave per sample (heads_sample); in training with `scalars`, the last workgroup to
-// finish (completion counter, release/acquire fences) runs the scalar reduction, so the step
-// needs no separate scalars launch.  No early return: every wave reaches the barriers.
+// finish (completion counter) runs the scalar reduction, so the step needs no separate scalars
+// launch.  No early return: every wave reaches the barriers.  Hand-off protocol (no fences, the
+// "every store sc1 / every load sc1" form of MI355X_MICROARCH.md §Correctness boundaries):
+// every handed-off word is written with an agent-scope store (st_agent: global_store sc1, which
+// leaves the XCD's L2) or a device atomic (ReLU counts); each wave drains its stores
+// (s_waitcnt 0) and the workgroup barriers BEFORE thread 0 increments the counter; the last
+// workgroup reads the words only with agent-scope loads (ld_agent: global_load sc1) after its
+// barrier.  The counter itself is a device atomic.  No step relies on release/acquire ordering.
 __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -204,14 +204,19 @@ def get_nn_prediction(params, state, cfg, explore_factor=1.0):
     x = state.astype(dt) / dt.type(255.0)                                     # train.py:167
     x = np.concatenate([x, np.zeros((B, 84, 84, TARGET_CHANNELS - C), dt)], axis=3)  # :173-174
     t = {"x": x}
-    a0 = relu(conv2d_valid(x, params["conv0/W"]))                          # :177-178,175
+    z0 = conv2d_valid(x, params["conv0/W"])                                 # :177-178
+    a0 = relu(z0)                                                           # :175
     p0, c0 = maxpool2x2_argmax(a0)                                          # :185
-    a1 = relu(conv2d_valid(p0, params["conv1/W"]))                          # :187-188
+    z1 = conv2d_valid(p0, params["conv1/W"])                                # :187-188
+    a1 = relu(z1)
     p1, c1 = maxpool2x2_argmax(a1)                                          # :195
-    a2 = relu(conv2d_valid(p1, params["conv2/W"]))                          # :197-198
+    z2 = conv2d_valid(p1, params["conv2/W"])                                # :197-198
+    a2 = relu(z2)
     p2, c2 = maxpool2x2_argmax(a2)                                          # :204
-    a3 = relu(conv2d_valid(p2, params["conv3/W"]))                          # :206-207
-    t.update(a0=a0, p0=p0, c0=c0, a1=a1, p1=p1, c1=c1, a2=a2, p2=p2, c2=c2, a3=a3)
+    z3 = conv2d_valid(p2, params["conv3/W"])                                # :206-207
+    a3 = relu(z3)
+    t.update(a0=a0, p0=p0, c0=c0, a1=a1, p1=p1, c1=c1, a2=a2, p2=p2, c2=c2, a3=a3,
+             z0=z0, z1=z1, z2=z2, z3=z3)
     flat = a3.reshape(B, 1600)                                              # batch_flatten
     F = cfg["fc_neurons"]
     if cfg.get("replace_with_conv", True):
@@ -241,14 +246,25 @@ def get_nn_prediction(params, state, cfg, explore_factor=1.0):
 
 # --- loss (train.py:274-327) ------------------------------------------------------------
 def build_graph_cost(params, state, action, futurereward, cfg, entropy_beta=0.01,
-                     frozen_advantage=None):
+                     frozen_advantage=None, forced_h=None):
     """Model._build_graph (`train.py:274-327`): returns (t, scalars) with t['cost'].
 
     `frozen_advantage` replaces stop_gradient(V) - R by a constant array, so a finite
     difference of `cost` sees exactly the function TF differentiates (`train.py:309`).
+    `forced_h` (tests only, replace_with_conv FC) evaluates the heads, softmax and loss on a
+    given FC output [B, F] — the checked side's own — so that the head / loss gradient is
+    compared on its arithmetic alone where the policy saturates: there d(dz)/dz is
+    exp-amplified and any fp32 forward (TF's included) moves dz by |dz| * |dlogit|.
     """
     t = get_nn_prediction(params, state, cfg)
     dt = params["conv0/W"].dtype
+    if forced_h is not None:
+        # the heads and the loss evaluated on the checked side's own FC output (tests only)
+        h = forced_h.astype(dt)
+        t["h"] = h
+        t["policy"] = h @ params["fc-pi/W"] + params["fc-pi/b"]
+        t["pred_value"] = (h @ params["fc-v/W"] + params["fc-v/b"])[:, 0]
+        t["logits"] = softmax(t["policy"])
     p = t["logits"]
     V = t["pred_value"]
     R = futurereward.astype(dt)
@@ -356,7 +372,10 @@ def loss_and_grads(params, state, action, futurereward, cfg, entropy_beta=0.01, 
     'a3_mask': bool} replaces the oracle's own max-pool / ReLU decisions in the backward pass,
     so an fp32 implementation can be compared on arithmetic alone when a near-tie or a
     pre-activation within rounding of zero resolves differently in fp32 and fp64."""
-    t, scalars = build_graph_cost(params, state, action, futurereward, cfg, entropy_beta)
+    fh = None if forced is None else forced.get("h")
+    assert fh is None or cfg.get("replace_with_conv", True), "forced h: identity FC only"
+    t, scalars = build_graph_cost(params, state, action, futurereward, cfg, entropy_beta,
+                                  forced_h=fh)
     t["R"] = futurereward.astype(params["conv0/W"].dtype)
     if forced is not None:
         t["forced"] = forced
@@ -371,11 +390,14 @@ def loss_and_grads_chunked(params, state, action, futurereward, cfg, entropy_bet
     the full-batch gradient is sum_c (B_c/B) grad_c, and the scalars combine the same way
     (means weighted, max_logit maxed, active_relus summed).  Returns (t, scalars, grads) with t
     holding the per-sample outputs ('logits', 'pred_value') and the oracle's own discrete
-    decisions ('own_c0'..'own_c2': argmax codes with 255 where the window max <= 0, 'a3_pos')."""
+    decisions ('own_c0'..'own_c2': argmax codes with 255 where the window max <= 0, 'a3_pos')
+    and where those decisions are numerically ambiguous ('near_c0'..'near_c2', 'near_a3', see
+    ambiguous_windows)."""
     B = state.shape[0]
     dt = params["conv0/W"].dtype
     grads, sc = None, None
-    keep = {"logits": [], "pred_value": [], "own_c0": [], "own_c1": [], "own_c2": [], "a3_pos": []}
+    keep = {"logits": [], "pred_value": [], "own_c0": [], "own_c1": [], "own_c2": [], "a3_pos": [],
+            "near_c0": [], "near_c1": [], "near_c2": [], "near_a3": []}
     for lo in range(0, B, chunk):
         hi = min(B, lo + chunk)
         f = None if forced is None else {k: v[lo:hi] for k, v in forced.items()}
@@ -399,8 +421,37 @@ def loss_and_grads_chunked(params, state, action, futurereward, cfg, entropy_bet
         keep["pred_value"].append(t["pred_value"])
         for layer in range(3):
             keep["own_c%d" % layer].append(np.where(t["p%d" % layer] > 0, t["c%d" % layer], 255))
+            keep["near_c%d" % layer].append(ambiguous_windows(t["z%d" % layer]))
         keep["a3_pos"].append(t["a3"] > 0)
+        keep["near_a3"].append(ambiguous_relu(t["z3"]))
     return {k: np.concatenate(v) for k, v in keep.items()}, sc, grads
+
+
+def _image_scale(z):
+    return np.abs(z).reshape(z.shape[0], -1).max(axis=1).reshape((-1,) + (1,) * (z.ndim - 1))
+
+
+def ambiguous_windows(z, tol=2e-5):
+    """Max-pool windows of the pre-ReLU conv output z [B,H,W,C] whose first-max / ReLU
+    decision an fp32 evaluation may legitimately resolve differently from this fp64 one: a
+    window max within tol * (the image's max |z|) of zero (but not exactly zero: an all-zero
+    patch is zero in any arithmetic), or a competitor that is NOT exactly
+    equal to the max but within that distance of it (a near-tie).  Exact ties are not
+    ambiguous: identical patches give identical values in any arithmetic.  Returns a bool mask
+    of the pooled shape [B,H/2,W/2,C]."""
+    B, H, W, C = z.shape
+    win = z.reshape(B, H // 2, 2, W // 2, 2, C).transpose(0, 1, 3, 5, 2, 4).reshape(B, H // 2, W // 2, C, 4)
+    eps = tol * _image_scale(z)[..., None]
+    m = win.max(axis=-1, keepdims=True)
+    gap = m - win
+    near_tie = ((gap > 0) & (gap <= eps)).any(axis=-1)
+    near_zero = (m[..., 0] != 0) & (np.abs(m[..., 0]) <= eps[..., 0])   # exact zeros: zero patches
+    return near_tie | near_zero
+
+
+def ambiguous_relu(z, tol=2e-5):
+    """Pre-activations within tol * (the image's max |z|) of zero (ReLU sign decision)."""
+    return (z != 0) & (np.abs(z) <= tol * _image_scale(z))
 
 
 # --- gradient processor (train.py:329-330, tfutils/gradproc.py:34-67) --------------------

@@ -176,10 +176,17 @@ def test_two_phase_backward_equals_one_pass(B):
     t, off = eng.bucket_split()
     assert eng.layout[t][0].startswith("fc1")
     mid = eng.grads.clone()
+    # The overlap contract of the bucketed exchange (trainer.py _bucketed_sync_step): while
+    # the bucket [off:] is being all-reduced, phase 2 must not write it at all — a sentinel
+    # there survives phase 2 — and must rewrite every conv gradient element [:off].
+    eng.grads[off:] = 7.25
+    eng.grads[:off] = -3.5
     sc1 = eng.train_grads(state, action, R, phase=2)
     torch.cuda.synchronize()
+    assert bool((eng.grads[off:] == 7.25).all())
     for i, (name, o, n, _) in enumerate(eng.layout):   # (the 64-float alignment gaps are not
         if i >= t:                                      # gradient elements)
             assert torch.equal(mid[o:o + n], ref[o:o + n]), name
-        assert torch.equal(eng.grads[o:o + n], ref[o:o + n]), name
+        else:
+            assert torch.equal(eng.grads[o:o + n], ref[o:o + n]), name
     assert torch.equal(sc1, sc)
