@@ -19,6 +19,7 @@
 #include "ba3c_band6.h"
 #include "ba3c_conv.h"
 #include "ba3c_gemm6.h"
+#include "ba3c_launch.h"
 #include "ba3c_multi.h"
 #include "ba3c_problems.h"
 #include "ba3c_rollout.h"
@@ -82,7 +83,7 @@ struct ba3c_handle {
   // give every workgroup whole images (conv_band6r_kernel; BA3C_RING=0: one band per workgroup)
   bool ring = true;
   int cus = 256;      // compute units of the device (persistent grids)
-  int c0lay = 2;      // conv0 forward LDS layout (ba3c_split.h; BA3C_C0LAY=0/1/2)
+  int c0lay = 3;      // conv0 forward LDS layout (ba3c_split.h; BA3C_C0LAY=2: r02's pairing)
   bool g6 = true;     // implicit-GEMM launches (conv3, fc1, heads; C=12 conv0) on bf16x6 split
                       // MFMA (ba3c_gemm6.h; BA3C_GEMM6=0 or BA3C_GENERIC=1: fp32 MFMA)
   // split family of the split kernels: 2 = scaled fp16 hi/lo, 3 MFMAs per fp32 product
@@ -572,7 +573,7 @@ int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, con
   const Conv0SArgs sa{state, reinterpret_cast<const uint4*>(w.wt + WT_C0S), w.p0, train ? w.c0 : nullptr,
                       train ? w.relu : nullptr, B, w.wexp + 4, w.am(AM_P0, h)};
   ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-  return launch_multi<false, Conv0SJob<NS, 2>, WPrep6Job<NS>>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)),
+  return launch_multi<false, Conv0SJob<NS, 3>, WPrep6Job<NS>>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)),
                                                               rest, dim3(64, rest.jobs.njobs));
 }
 
@@ -621,9 +622,7 @@ int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a, const Wo
                         a.relu_count, a.batch, w.wexp + 4, w.am(AM_P0, h)};
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
     const dim3 grid(std::min(FW_P0S, a.batch * Conv0S::NBANDS));
-    if (h->c0lay == 2) hipLaunchKernelGGL((conv0s_fwd_kernel<NS, 2>), grid, dim3(256), 0, s, sa);
-    else if (h->c0lay == 1) hipLaunchKernelGGL((conv0s_fwd_kernel<NS, 1>), grid, dim3(256), 0, s, sa);
-    else hipLaunchKernelGGL((conv0s_fwd_kernel<NS, 0>), grid, dim3(256), 0, s, sa);
+    HIP_TRY(launch_conv0s_fwd(NS, h->c0lay, grid, s, sa));   // ba3c_conv0.hip
   } else {
     ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
     hipLaunchKernelGGL(conv0_band_kernel, dim3(a.batch * Conv0Geom::NBANDS), dim3(256), 0, s, a);
@@ -649,7 +648,7 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   // small batches on the split path: weight prep beside conv0's forward (one launch fewer on
   // the critical path)
   const bool mj = h->multi && B <= OVERLAP_B && CH == 4 && h->band && h->b6 && h->split && NS == 2 &&
-                  h->c0lay == 2;
+                  h->c0lay == 3;
   if (mj) CHECK(launch_prep_conv0_multi<NS>(h, s, prm, state, B, w, train));
   else if (h->band) CHECK(launch_wprep<NS>(h, s, prm, w, train));
   if (train) {
@@ -973,8 +972,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     const int P = std::min(WG_P0S, B * Conv0W<NS>::NBANDS);
     {
       ProbeScope ps(h, s, BA3C_K_CONV0_WGRAD);
-      hipLaunchKernelGGL(conv0s_wgrad_kernel<NS>, dim3(P), dim3(256), 0, s,
-                         Conv0WArgs{state, w.dp0, w.c0, w.part0, B, w.am(AM_DP0, h)});
+      HIP_TRY(launch_conv0s_wgrad(NS, dim3(P), s, Conv0WArgs{state, w.dp0, w.c0, w.part0, B, w.am(AM_DP0, h)}));
     }
     HIP_TRY(hipGetLastError());
     ReduceMap mp{};
@@ -1095,7 +1093,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
       h->cus = n;
   }
-  if (const char* e = getenv("BA3C_C0LAY")) h->c0lay = std::max(0, std::min(2, atoi(e)));
+  if (const char* e = getenv("BA3C_C0LAY")) h->c0lay = atoi(e) == 2 ? 2 : 3;
   if (const char* e = getenv("BA3C_GEMM6")) h->g6 = !(e[0] == '0');
   if (!h->band) h->g6 = false;
   if (const char* e = getenv("BA3C_SPLIT")) h->ns = (std::strcmp(e, "bf16") == 0) ? 3 : 2;

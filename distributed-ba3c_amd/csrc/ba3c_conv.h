@@ -243,6 +243,7 @@ struct Conv0Geom {
   static constexpr int MCH = 10;                            // m-blocks per register chunk
 };
 
+#if BA3C_SHARED_KERNELS  // non-template kernel: emitted by ba3c_capi.hip only
 __global__ void __launch_bounds__(256) conv0_band_kernel(const BandArgs a) {
   using G = Conv0Geom;
   __shared__ float4 xs4[G::SROWS * G::WS];
@@ -332,8 +333,10 @@ __global__ void __launch_bounds__(256) conv0_band_kernel(const BandArgs a) {
   }
   if (a.relu_count) relu_count_add(a.relu_count, pos, lane);
 }
+#endif
 
 // conv0 weights as [32][112]: k = (tap, c) for taps < 25 of the real channels, zero beyond
+#if BA3C_SHARED_KERNELS  // non-template kernel: emitted by ba3c_capi.hip only
 __global__ void __launch_bounds__(256) conv0_wprep_kernel(const float* __restrict__ w,
                                                           float* __restrict__ wt) {
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -343,6 +346,7 @@ __global__ void __launch_bounds__(256) conv0_wprep_kernel(const float* __restric
   // conv0/W is [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99); real channels c < 4
   wt[e] = tap < Conv0Geom::NTAP ? w[((size_t)tap * 16 + c) * 32 + o] : 0.f;
 }
+#endif
 
 // ---------------------------------------------------------------------------------------
 // Per-step weight preparation: B operand of a band conv as [N][K] with K = (kh, kw, c).
@@ -374,9 +378,11 @@ __device__ __forceinline__ float wprep_value(const WPrepJob& j, int e) {
   return j.w[((size_t)(kh * j.KW + kw) * j.CI + ci) * j.CO + o];
 }
 
+#if BA3C_SHARED_KERNELS  // non-template kernel: emitted by ba3c_capi.hip only
 __global__ void __launch_bounds__(256) wprep_kernel(const WPrepArgs a) {
   const WPrepJob& j = a.job[blockIdx.y];
   for (int e = blockIdx.x * 256 + threadIdx.x; e < j.n; e += gridDim.x * 256) j.wt[e] = wprep_value(j, e);
 }
+#endif
 
 }  // namespace ba3c

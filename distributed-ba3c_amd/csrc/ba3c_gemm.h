@@ -18,6 +18,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Non-template kernels defined in the shared headers are emitted by one translation unit only
+// (ba3c_capi.hip); the other units (ba3c_conv0.hip) set this to 0.
+#ifndef BA3C_SHARED_KERNELS
+#define BA3C_SHARED_KERNELS 1
+#endif
+
 namespace ba3c {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));

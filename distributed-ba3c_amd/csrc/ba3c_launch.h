@@ -1,0 +1,16 @@
+// ba3c_launch.h — host launchers of kernels that live in their own translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ba3c {
+
+struct Conv0SArgs;
+struct Conv0WArgs;
+
+// conv0 forward (persistent bands, ba3c_split.h), split family ns (2 fp16 / 3 bf16), LDS
+// layout lay (2 or 3); returns hipGetLastError() of the launch
+hipError_t launch_conv0s_fwd(int ns, int lay, dim3 grid, hipStream_t s, const Conv0SArgs& a);
+// conv0 weight gradient partial slabs (ba3c_split.h)
+hipError_t launch_conv0s_wgrad(int ns, dim3 grid, hipStream_t s, const Conv0WArgs& a);
+
+}  // namespace ba3c

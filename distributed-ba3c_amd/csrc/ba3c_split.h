@@ -142,7 +142,7 @@ struct Conv0S {
   static constexpr int HO = 80, WO = 80, RB = 16, NBANDS = HO / RB, SROWS = RB + KT - 1;
   static constexpr int KSTEPS = 4;                 // 4 x 32 K = 32 tap slots (25 used)
   // LDS row pitch (pixels) of layout LAY: 0 = dense 84 with taps in order (r01), 1 = 88 with
-  // taps in order, 2 = 88 with the paired tap order (conv0_atap); 704 B = 64 mod 256
+  // taps in order, 2 / 3 = 88 with the paired tap orders (conv0_atap); 704 B = 64 mod 256
   __host__ __device__ static constexpr int xp(int lay) { return lay ? 88 : 84; }
   static constexpr int MAXSPLIT = 3;
   static constexpr int PROWS_W = RB / 2 / 4;       // pooled rows per wave (2)
@@ -165,13 +165,24 @@ struct Conv0S {
 __host__ __device__ constexpr int conv0_pair(int s, int q, int h) { return 4 * s + 2 * (q >> 1) + h; }
 // the tap whose pixels slot (s, q, h) reads (always a real tap: in-bounds, finite values);
 // layouts 0 / 1 keep the plain order tap = 8s + 2q + h (padding slots read tap 0)
+//
+// Layout 3 (default): the two taps of a LANE's A fragment are (t, t + 10) = (kh, kw) and
+// (kh + 2, kw), two LDS rows apart for every lane and k-step, so the fragment is ONE
+// ds_read2_b64 into four consecutive VGPRs (r02's layout 2 needed two reads whose registers
+// the compiler then copied together: ~3 v_mov per fragment).  Pair P = 4s + q: P < 10 holds
+// taps (P, P + 10); P = 10..14 holds (P, P + 10) with the first half padding (weight 0, reads
+// the in-band row kh = 2) and the second the kh = 4 tap; P = 15 is padding in both halves.
+// A 16-lane group reads 2 rows x 8 pixels of 8 B; with the 88-pixel pitch (704 B = 64 mod 128)
+// those 16 addresses are distinct mod 128 B: conflict-free for ds_read2_b64's 4 x 16 groups.
 __host__ __device__ constexpr int conv0_atap(int s, int q, int h, int lay = 2) {
-  return lay == 2 ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) : 0) + 10 * (q & 1)
+  return lay == 3 ? (4 * s + q < 15 ? 4 * s + q : 0) + 10 * h
+       : lay == 2 ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) : 0) + 10 * (q & 1)
                   : (8 * s + 2 * q + h < 25 ? 8 * s + 2 * q + h : 0);
 }
 // the tap whose weight slot (s, q, h) carries, -1 for padding
 __host__ __device__ constexpr int conv0_wtap(int s, int q, int h, int lay = 2) {
-  return lay == 2 ? ((q & 1) ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) + 10 : -1)
+  return lay == 3 ? (4 * s + q < 10 ? 4 * s + q + 10 * h : (4 * s + q < 15 && h ? 4 * s + q + 10 : -1))
+       : lay == 2 ? ((q & 1) ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) + 10 : -1)
                              : (conv0_pair(s, q, h) < 10 ? conv0_pair(s, q, h) : -1))
                   : (8 * s + 2 * q + h < 25 ? 8 * s + 2 * q + h : -1);
 }
@@ -221,10 +232,12 @@ __device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, ui
                    part[sp][4] | (part[sp][5] << 16), part[sp][6] | (part[sp][7] << 16));
 }
 
+#if BA3C_SHARED_KERNELS  // non-template kernel: emitted by ba3c_capi.hip only
 __global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restrict__ w,
                                                            uint4* __restrict__ wb, int lay) {
   conv0s_wprep_one<3>(w, wb, blockIdx.x * 256 + threadIdx.x, 0, lay);
 }
+#endif
 
 // Persistent workgroups walk bands (one image x RB output rows = RB/2 pooled rows); wave w
 // owns pooled rows 2w, 2w+1 of a band = 20 m-blocks of 4 windows, both 16-channel n-tiles.
@@ -251,13 +264,66 @@ __device__ __forceinline__ uint32_t u8pair(uint32_t a, uint32_t b) {
   else return pack_f16x2((float)a, (float)b);
 }
 
+// Layout 3 stores every 16-bit pixel twice: LDS entry (r, x) is 16 bytes [pixel (r, x) |
+// pixel (r + 2, x)] (rows of the band, 4 channels each), so a lane's A fragment of taps
+// (t, t + 10) is ONE aligned ds_read_b128 (two 8-byte reads let the compiler pair halves of
+// different m-blocks and re-copy them: ~3 v_mov per fragment).  Entry rows 0 .. SROWS-3 are
+// read (row r + kh, kh <= 2); the entry pitch 88 (= 8 mod 16 entries) puts a 16-lane group's
+// two output rows in disjoint bank halves.
+constexpr int C0E_ROWS = Conv0S::SROWS - 2, C0E_PITCH = 88;
+// four frame bytes (one pixel's 4 channels) -> two packed 16-bit pairs of the split family.
+// fp16: 0x6400 | b is 1024 + b exactly, so one v_perm_b32 per pair builds the magic values and
+// one v_pk_add_f16 of -1024 leaves b exactly (bits identical to a float conversion)
+template <int NS>
+__device__ __forceinline__ void u8quad(uint32_t px, uint32_t& o01, uint32_t& o23) {
+  if constexpr (NS == 3) {
+    o01 = u8pair<NS>(px & 255u, (px >> 8) & 255u);
+    o23 = u8pair<NS>((px >> 16) & 255u, px >> 24);
+  } else {
+    const f16x2v m1024 = {(_Float16)-1024.0f, (_Float16)-1024.0f};
+    const uint32_t k = 0x64646464u;
+    const f16x2v a = __builtin_bit_cast(f16x2v, __builtin_amdgcn_perm(k, px, 0x04010400u)) + m1024;
+    const f16x2v b = __builtin_bit_cast(f16x2v, __builtin_amdgcn_perm(k, px, 0x04030402u)) + m1024;
+    o01 = __builtin_bit_cast(uint32_t, a);
+    o23 = __builtin_bit_cast(uint32_t, b);
+  }
+}
+
 template <int LAY>
-constexpr int conv0s_fwd_lds_bytes() { return Conv0S::SROWS * Conv0S::xp(LAY) * 8; }
+constexpr int conv0s_band_bytes() {
+  return LAY == 3 ? C0E_ROWS * C0E_PITCH * 16 : Conv0S::SROWS * Conv0S::xp(LAY) * 8;
+}
+// per wave: one pooled row of the band's output (40 windows x 32 channels) as fp32 + codes,
+// staged so the global stores are whole 16-byte pieces (see the epilogue)
+constexpr int C0_WST_BYTES = (Conv0S::WO / 2) * Conv0S::COUT * 5;
+template <int LAY>
+constexpr int conv0s_fwd_lds_bytes() { return conv0s_band_bytes<LAY>() + 4 * C0_WST_BYTES; }
+
+// raw buffer resource over `base` (gfx9 descriptor word 3; offsets stay < 2^31 bytes)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+// ReLU positive test of an fp32 value by its bits as a signed integer: bits > 0 exactly for
+// x > 0 (+0 -> 0, negatives -> 0; -0 cannot come out of an accumulator that starts at +0).
+// Compiler-visible code only: an inline-asm v_med3_i32 here read MFMA results without the
+// wait states the hazard recognizer inserts for real VALU instructions (r03f: a stale ReLU
+// count), so the compiler's compare + carry-add form stays.
+__device__ __forceinline__ int pos01(int bits) { return bits > 0 ? 1 : 0; }
 
 // bx / gx: first band and persistent stride (blockIdx.x / gridDim.x of a plain launch);
 // lds: conv0s_fwd_lds_bytes<LAY>() bytes
+template <int NS, int LAY = 2, bool TRAIN = true>
+__device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, int gx, char* lds);
+
 template <int NS, int LAY = 2>
 __device__ __forceinline__ void conv0s_fwd_body(const Conv0SArgs& a, int bx, int gx, char* lds) {
+  // training (codes + ReLU count) and predictor variants: no per-store branch in the loop
+  if (a.out_code) conv0s_fwd_body_t<NS, LAY, true>(a, bx, gx, lds);
+  else conv0s_fwd_body_t<NS, LAY, false>(a, bx, gx, lds);
+}
+
+template <int NS, int LAY, bool TRAIN>
+__device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, int gx, char* lds) {
   using G = Conv0S;
   constexpr int XP = G::xp(LAY);
   using SP = SplitP<NS>;
@@ -265,34 +331,61 @@ __device__ __forceinline__ void conv0s_fwd_body(const Conv0SArgs& a, int bx, int
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbands = a.batch * G::NBANDS;
 
-  // ---- rows [y0, y0 + SROWS) of a band: contiguous 16-byte loads (4 pixels) ----
-  constexpr int NV = G::SROWS * G::WS / 4;         // 420 uint4
+  // ---- rows [y0, y0 + SROWS) of a band ----
+  // layouts 0-2: contiguous 16-byte loads (4 pixels), converted and stored as one run.
+  // Layout 3: one thread per 16-byte ENTRY (r, x) = [pixel (r, x) | pixel (r + 2, x)]: two dword
+  // loads (coalesced over consecutive x), one ds_write_b128 — consecutive lanes write
+  // consecutive entries, conflict-free (r03e PMC: the 4-pixel runs written as 8-byte halves at a
+  // 64-byte lane stride made 52 % of the LDS cycles bank conflicts)
+  constexpr int NV = LAY == 3 ? C0E_ROWS * G::WS : G::SROWS * G::WS / 4;   // entries / uint4
   constexpr int NPT = (NV + 255) / 256;
-  uint4 v[NPT];
+  uint4 v[LAY == 3 ? 1 : NPT];
+  uint32_t ev[LAY == 3 ? NPT : 1][2];
   auto load_band = [&](int band) {
     const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
-    const uint4* src = reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
+    if constexpr (LAY == 3) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
 #pragma unroll
-    for (int i = 0; i < NPT; ++i) {
-      const int f = tid + 256 * i;
-      v[i] = f < NV ? src[f] : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < NPT; ++i) {
+        const int e = tid + 256 * i;               // entry e = row r * 84 + x: pixel index e
+        ev[i][0] = e < NV ? src[e] : 0u;
+        ev[i][1] = e < NV ? src[e + 2 * G::WS] : 0u;
+      }
+    } else {
+      const uint4* src = reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int f = tid + 256 * i;
+        v[i] = f < NV ? src[f] : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto store_band = [&]() {
+    if constexpr (LAY == 3) {
 #pragma unroll
-    for (int i = 0; i < NPT; ++i) {
-      const int f = tid + 256 * i;
-      if (f < NV) {
-        const uint32_t px[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-        uint32_t o[8];
+      for (int i = 0; i < NPT; ++i) {
+        const int e = tid + 256 * i;
+        if (e < NV) {
+          const int r = e / G::WS, x = e - r * G::WS;
+          uint32_t o[4];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          o[2 * p] = u8pair<NS>(px[p] & 255u, (px[p] >> 8) & 255u);
-          o[2 * p + 1] = u8pair<NS>((px[p] >> 16) & 255u, px[p] >> 24);
+          for (int h = 0; h < 2; ++h) u8quad<NS>(ev[i][h], o[2 * h], o[2 * h + 1]);
+          reinterpret_cast<uint4*>(lds)[r * C0E_PITCH + x] = make_uint4(o[0], o[1], o[2], o[3]);
         }
-        const int px0 = 4 * f, r = px0 / G::WS, lp = r * XP + (px0 - r * G::WS);   // 4 px of one row
-        reinterpret_cast<uint4*>(xs + lp)[0] = make_uint4(o[0], o[1], o[2], o[3]);
-        reinterpret_cast<uint4*>(xs + lp)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int f = tid + 256 * i;
+        if (f < NV) {
+          const uint32_t px[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+          uint32_t o[8];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) u8quad<NS>(px[p], o[2 * p], o[2 * p + 1]);
+          const int px0 = 4 * f, r = px0 / G::WS, lp = r * XP + (px0 - r * G::WS);   // 4 px of one row
+          reinterpret_cast<uint4*>(xs + lp)[0] = make_uint4(o[0], o[1], o[2], o[3]);
+          reinterpret_cast<uint4*>(xs + lp)[1] = make_uint4(o[4], o[5], o[6], o[7]);
+        }
       }
     }
   };
@@ -313,28 +406,45 @@ __device__ __forceinline__ void conv0s_fwd_body(const Conv0SArgs& a, int bx, int
       }
   // this lane's row (window li>>2, sub li&3) of m-block 0 of the wave, per (kstep, tap half)
   const int wi = li >> 2, sub = li & 3;
-  const int pix0 = (4 * wave + (sub >> 1)) * XP + 2 * wi + (sub & 1);
+  // (layout 3: entry index, pitch C0E_PITCH; else pixel index, pitch XP)
+  constexpr int RP = LAY == 3 ? C0E_PITCH : XP;
+  const int pix0 = (4 * wave + (sub >> 1)) * RP + 2 * wi + (sub & 1);
   int lb[G::KSTEPS][2];
 #pragma unroll
   for (int s = 0; s < G::KSTEPS; ++s)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int tap = conv0_atap(s, lq, h, LAY);
-      lb[s][h] = pix0 + (tap / G::KT) * XP + tap % G::KT;
+      lb[s][h] = pix0 + (tap / G::KT) * RP + tap % G::KT;
     }
 
-  unsigned long long pos = 0;
+  int pos = 0;                                      // this lane's ReLU positives (TRAIN)
   // (sum_k u8 * w 2^kw) * (2^-kw / 255): scaling by a power of two commutes with the rounding
   const float oscale = NS == 2 ? (1.0f / 255.0f) * exp2i(-a.wexp[0]) : 1.0f / 255.0f;
+  // Epilogue stores go through a wave-private LDS area holding one pooled row of outputs
+  // (40 windows x 32 channels: 5 KB fp32 + 1.25 KB codes, contiguous in global memory too):
+  // each lane writes its window / channel values there, then the wave copies the row out in
+  // 16-byte pieces, consecutive lanes consecutive pieces — 7 buffer_store_dwordx4 per pooled
+  // row instead of 40 dword + 40 byte stores (r03i: a byte store per value cost ~7 cycles of
+  // the CU's store path each)
+  float* wst = reinterpret_cast<float*>(lds + conv0s_band_bytes<LAY>() + wave * C0_WST_BYTES);
+  uint8_t* wsc = reinterpret_cast<uint8_t*>(wst + (G::WO / 2) * G::COUT);
+  const int lane_el = lq * G::COUT + li;           // (window lq, channel li) in the row area
   for (; band < nbands; band += gx) {
     const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
     __syncthreads();                                 // previous band's LDS reads are done
     store_band();
     __syncthreads();
     if (band + gx < nbands) load_band(band + gx);
-    float bmax = 0.f;
+    const size_t band_el = (size_t)(img * (G::HO / 2) + y0 / 2) * (G::WO / 2) * G::COUT;
+    int bmaxi = 0;                                  // max window-max bits of the band
 #pragma unroll
     for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
+      // chunks do not overlap inside a wave (the two waves per SIMD overlap each other's
+      // epilogue and MFMAs): without this fence the scheduler interleaves chunk c + 1's A reads
+      // and MFMAs with chunk c's epilogue, two accumulator sets live -> > 256 registers and one
+      // wave per SIMD (r03g: 0.35 ms)
+      __builtin_amdgcn_sched_barrier(0);
       f32x4 acc[G::MCH][2];
 #pragma unroll
       for (int j = 0; j < G::MCH; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -344,9 +454,15 @@ __device__ __forceinline__ void conv0s_fwd_body(const Conv0SArgs& a, int bx, int
 #pragma unroll
         for (int j = 0; j < G::MCH; ++j) {
           const int jj = ch * G::MCH + j;
-          const int off = (jj / G::MBROW) * 2 * XP + (jj % G::MBROW) * 8;   // immediate
-          const uint2 p0 = xs[lb[s][0] + off], p1 = xs[lb[s][1] + off];
-          af[j] = u32x4{p0.x, p0.y, p1.x, p1.y};
+          const int off = (jj / G::MBROW) * 2 * RP + (jj % G::MBROW) * 8;   // immediate
+          if constexpr (LAY == 3) {
+            // both taps of the fragment in one 16-byte entry: one ds_read_b128
+            const uint4 u = reinterpret_cast<const uint4*>(lds)[lb[s][0] + off];
+            af[j] = u32x4{u.x, u.y, u.z, u.w};
+          } else {
+            const uint2 p0 = xs[lb[s][0] + off], p1 = xs[lb[s][1] + off];
+            af[j] = u32x4{p0.x, p0.y, p1.x, p1.y};
+          }
         }
 #pragma unroll
         for (int sp = 0; sp < NS; ++sp)
@@ -356,32 +472,63 @@ __device__ __forceinline__ void conv0s_fwd_body(const Conv0SArgs& a, int bx, int
             for (int j = 0; j < G::MCH; ++j)
               acc[j][nt] = SP::mfma(af[j], wf[sp][nt][s], acc[j][nt]);
       }
-      // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nt*16 + li
+      // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nt*16 + li.
+      // Max of the ReLU'd window = max(v0..v3, +0), taken on the fp32 BITS as signed
+      // integers (negative values are negative integers, positive ones order like floats;
+      // integer max needs no NaN canonicalisation): two v_max3_i32.  Its argmax = the FIRST
+      // k with v_k == max (TF's strict-'<' update, models/pool.py:14-33); 255 when max <= 0.
 #pragma unroll
       for (int j = 0; j < G::MCH; ++j) {
         const int jj = ch * G::MCH + j;
-        const int ph = y0 / 2 + 2 * wave + jj / G::MBROW;
-        const int pw = 4 * (jj % G::MBROW) + lq;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const float v0 = acc[j][nt][0], v1 = acc[j][nt][1], v2 = acc[j][nt][2], v3 = acc[j][nt][3];
-          pos += count_pos4(v0, v1, v2, v3);   // wave-uniform
-          float mx = v0;
-          uint32_t arg = 0;
-          if (v1 > mx) { mx = v1; arg = 1; }
-          if (v2 > mx) { mx = v2; arg = 2; }
-          if (v3 > mx) { mx = v3; arg = 3; }
-          const size_t o = ((size_t)(img * (G::HO / 2) + ph) * (G::WO / 2) + pw) * G::COUT + nt * 16 + li;
-          const float out = mx > 0.f ? mx * oscale : 0.f;
-          bmax = fmaxf(bmax, out);
-          a.out[o] = out;
-          if (a.out_code) a.out_code[o] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+          // element of (window 4 (jj % 10), n-tile) in the row area, from lane_el
+          const int cofs = 4 * (jj % G::MBROW) * G::COUT + nt * 16;
+          const int b0 = __float_as_int(acc[j][nt][0]), b1 = __float_as_int(acc[j][nt][1]);
+          const int b2 = __float_as_int(acc[j][nt][2]), b3 = __float_as_int(acc[j][nt][3]);
+          const int m = max(max(max(b0, b1), b2), max(b3, 0));
+          bmaxi = max(bmaxi, m);
+          wst[lane_el + cofs] = __int_as_float(m) * oscale;
+          if constexpr (TRAIN) {
+            uint32_t arg = b2 == m ? 2u : 3u;
+            arg = b1 == m ? 1u : arg;
+            arg = b0 == m ? 0u : arg;
+            wsc[lane_el + cofs] = (uint8_t)(m != 0 ? arg : 255u);
+            pos += pos01(b0) + pos01(b1) + pos01(b2) + pos01(b3);
+            // materialise the count here: otherwise it is sunk to its only use after the band
+            // loop, keeping every accumulator of the chunk live (r03g: > 256 registers)
+            asm volatile("" : "+v"(pos));
+          }
+        }
+      }
+      if (ch % 2 == 1) {
+        // the wave's pooled row 2 wave + ch / 2 is complete in its LDS area: copy it out
+        const size_t row_el = band_el + (size_t)(2 * wave + ch / 2) * (G::WO / 2) * G::COUT;
+        const __amdgpu_buffer_rsrc_t rout = buf_rsrc(a.out + row_el);
+        constexpr int NF = (G::WO / 2) * G::COUT * 4 / 16;     // 320 pieces of 16 B
+#pragma unroll
+        for (int i = 0; i < NF / 64; ++i) {
+          const uint4 v = reinterpret_cast<const uint4*>(wst)[lane + 64 * i];
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rout, 16 * (lane + 64 * i), 0, 0);
+        }
+        if constexpr (TRAIN) {
+          const __amdgpu_buffer_rsrc_t rcode = buf_rsrc(a.out_code + row_el);
+          constexpr int NC = (G::WO / 2) * G::COUT / 16;       // 80 pieces of 16 B
+#pragma unroll
+          for (int i = 0; i < (NC + 63) / 64; ++i) {
+            const int piece = lane + 64 * i;
+            if (piece < NC) {
+              const uint4 v = reinterpret_cast<const uint4*>(wsc)[piece];
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rcode, 16 * piece, 0, 0);
+            }
+          }
         }
       }
     }
-    if constexpr (NS == 2) amax_publish(a.amax_out, img, bmax, lane);
+    // max over the window maxima, then the scale: a positive scale is monotone in fp32
+    if constexpr (NS == 2) amax_publish(a.amax_out, img, __int_as_float(bmaxi) * oscale, lane);
   }
-  if (a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
+  if (TRAIN && a.relu_count) relu_count_add(a.relu_count, (unsigned long long)pos, lane);
 }
 
 template <int NS, int LAY = 2>

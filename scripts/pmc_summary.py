@@ -75,6 +75,8 @@ def main():
             "SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT",
             "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS", "SQ_LDS_UNALIGNED_STALL", "SQ_WAVE_CYCLES",
             "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]
+    extra = sorted({c for cs in res.values() for c in cs} - set(cols))
+    cols = [c for c in cols if any(c in cs for cs in res.values())] + extra
     print("| kernel | " + " | ".join(cols) + " |")
     print("|---" * (len(cols) + 1) + "|")
     for k in sorted(res):
