@@ -183,6 +183,49 @@ def overlap_bench(tr, batch, pred_batch, iters, world):
             "predict_states_per_s": round(world * pred_batch / (t_pred / 1000.0), 1)}
 
 
+def exchange_bench(tr, batch, iters, world, ms_step):
+    """N > 1: where the data-parallel exchange's time goes, per rank (max over ranks).
+    `local_step_ms` is the same bucketed step with the two RCCL sums left out (each rank clips
+    and applies its own gradients), `allreduce_ms` the two bucket sums run alone, so
+    `exposed_ms` = step - local is what the exchange adds to the step and `hidden_frac` how
+    much of the all-reduce time the conv backward covers (trainer.py:_bucketed_sync_step).
+    Runs after the timed region (replicas diverge while the exchange is off)."""
+    opt, eng = tr.optimizer, tr.engine
+    tb, off = eng.bucket_split()
+    total = eng.grads.numel()
+
+    def timed(fn):
+        sync_all(world)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        sync_all(world)
+        return (time.perf_counter() - t0) / iters * 1000.0
+
+    def ar(lo, hi):
+        w = opt._all_reduce(eng.grads[lo:hi], async_op=True)
+        if w is not None:
+            w.wait()
+
+    t_big = timed(lambda: ar(off, total))
+    t_small = timed(lambda: ar(0, off))
+    opt.distributed = False
+    try:
+        t_local = timed(lambda: tr.train_step(*batch))
+    finally:
+        opt.distributed = True
+    el = torch.tensor([t_big, t_small, t_local], dtype=torch.float64, device="cuda")
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    t_big, t_small, t_local = (float(x) for x in el.tolist())
+    exposed = ms_step - t_local
+    return {"buckets": {"fc1_heads": {"bytes": 4 * (total - off), "allreduce_ms": round(t_big, 4)},
+                        "conv": {"bytes": 4 * off, "allreduce_ms": round(t_small, 4)}},
+            "backend": dist.get_backend(), "local_step_ms": round(t_local, 4),
+            "step_ms": round(ms_step, 4), "exposed_ms": round(exposed, 4),
+            "hidden_frac": round(1.0 - max(exposed, 0.0) / max(t_big + t_small, 1e-9), 3),
+            "iters": iters}
+
+
 def find_dominant_kernel(tr, batch):
     from ba3c_amd._lib import KERNEL_IDS
     eng = tr.engine
@@ -247,7 +290,7 @@ def cpu_baseline(F, S, A, big_seconds=10.0, b32_steps=50):
             ts.append(time.perf_counter() - t0)
         return float(np.median(ts)), len(ts)
 
-    big_med, big_n = run(2048, F, S, 2, 20, big_seconds, 1)
+    big_med, big_n = run(2048, F, S, 5, 20, big_seconds, 1)
     small_med, small_n = run(32, 128, 4, b32_steps, b32_steps, 0.0, 3)
     return {"value": round(2048 / big_med, 2), "unit": "samples/s", "cores": threads,
             "kind": "port",
@@ -271,7 +314,9 @@ def main():
     ap.add_argument("--no-b32", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--predict_batch", type=int, default=8192)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -280,9 +325,15 @@ def main():
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d (launch N>1 with torch.distributed.run)"
                          % (args.gpus, world))
+    if args.dist_backend == "gloo":
+        # rehearsal of N ranks on fewer GPUs: the exchange goes through a host copy
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     B, F, S, A = args.batch, args.fc_neurons, args.fc_splits, args.num_actions
     tr, batch = build_trainer(B, F, S, A, world, seed=rank)
@@ -341,6 +392,8 @@ def main():
            "roofline": roof,
            "kernel_ms_one_step": {k: round(v, 4) for k, v in per_kernel.items()}}
 
+    if world > 1:
+        out["exchange"] = exchange_bench(tr, batch, max(args.steps // 2, 5), world, ms_step)
     if not args.no_overlap:
         out["overlap"] = overlap_bench(tr, batch, args.predict_batch, 10, world)
     if not args.no_b32:
