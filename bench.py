@@ -341,6 +341,8 @@ def main():
         tr.train_step(*batch)
     sync_all(world)
     dom, per_kernel = find_dominant_kernel(tr, batch)
+    # A/B runs: time a named kernel over the timed steps instead of the dominant one
+    dom = os.environ.get("BA3C_BENCH_PROBE", dom)
     sync_all(world)
 
     elapsed, med_ms = time_steps(tr, batch, args.steps, args.warmup, world, probe=dom)

@@ -33,11 +33,20 @@ namespace ba3c {
 // With KPH < CIN the band is staged in CIN/KPH channel phases through the same LDS (smaller
 // footprint => more workgroups per CU to hide the staging); accumulators persist across
 // phases, so a phased layout needs all of a wave's m-blocks in one chunk.
-template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0, int NS_ = 3, bool DBUF_ = false>
+template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0, int NS_ = 3, bool DBUF_ = false,
+          bool TILE4_ = false>
 struct Band6 {
   // DBUF: A fragments of k-step t + 1 read into a second register set before k-step t's
   // MFMAs (only where the registers allow it without spilling)
   static constexpr bool DBUF = DBUF_;
+  // TILE4 (input-gradient layouts with 4-row bands): an m-block is a 4 x 4 pixel tile (rows
+  // 0..3 of the band x 4 columns) instead of 16 consecutive pixels, and the two waves of an
+  // n-block take tiles 0..4 / 5..9 of the band.  The input gradient is a VALID conv over the
+  // zero-padded un-pooled dY, so whole taps of a tile read only padding: kw = 0 for the left
+  // edge tile, kw = KW-1 for the right one, kh = 0 / KH-1 for every tile of the first / last
+  // band.  Those MFMAs multiply exact zeros and are not issued (8 % of conv1's input-gradient
+  // MFMAs); an MFMA adds its products to the accumulator exactly, so nothing else changes.
+  static constexpr bool TILE4 = TILE4_;
   using G = G_;
   static constexpr int NS = NS_;                         // split planes (3 bf16 / 2 fp16)
   static constexpr int KPH = KPH_ ? KPH_ : G_::CIN;
@@ -52,6 +61,12 @@ struct Band6 {
                 PP >= NS * SPB, "band6 layout");
   static_assert(NPH == 1 || NCH == 1, "phased staging keeps every accumulator live");
   static_assert(LDS_BYTES <= 160 * 1024, "band6 LDS");
+  static_assert(!TILE4 || (!G::POOL && G::SRC == 1 && G::RB == 4 && G::WO % 4 == 0 &&
+                           G::MB == 2 * G::MBW && G::WPN == 2 && NCH == 1 &&
+                           G::WO / 4 == G::MB && G::HO % 4 == 0 && G::PADX == G::KW - 1 &&
+                           G::PADY == G::KH - 1 && G::UWO + 2 * G::PADX == G::WS &&
+                           G::UHO + 2 * G::PADY == G::HS),
+                "4x4 tiles: input-gradient bands of 4 rows, one m-block chunk per wave");
 };
 
 struct Band6Args {
@@ -155,11 +170,25 @@ struct Band6Ops {
   __device__ static void compute(const Band6Args& a, const char* lds, int wave, int lane, int img, int y0,
                                  int rows_out, float us1, float us2, unsigned long long& pos, float& omax,
                                  StageFn&& stage_phase) {
+    if constexpr (L::TILE4) {
+      // the wave's edge tile (left for waves of tiles 0..4, right for 5..9) is compile-time
+      if (wave / G::NB == 0) compute_t<0>(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, stage_phase);
+      else compute_t<1>(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, stage_phase);
+    } else {
+      compute_t<0>(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, stage_phase);
+    }
+  }
+  template <int MB0, class StageFn>
+  __device__ static void compute_t(const Band6Args& a, const char* lds, int wave, int lane, int img, int y0,
+                                   int rows_out, float us1, float us2, unsigned long long& pos, float& omax,
+                                   StageFn&& stage_phase) {
     // lane-derived addressing goes through an empty asm: recomputed per band (a few VALU)
     // instead of being hoisted out of a persistent caller's band loop into live registers
     asm volatile("" : "+v"(lane));
     const int nb = wave % G::NB;
-    const int mb0 = wave / G::NB;
+    const int mb0 = L::TILE4 ? MB0 : wave / G::NB;
+    // TILE4: tap row kh_skip reads only padding for every tile of this band (-1: none)
+    const int kh_skip = !L::TILE4 ? -1 : (y0 == 0 ? 0 : (y0 + G::RB == G::HO ? G::KH - 1 : -1));
     const int li = lane & 15, lq = lane >> 4;
     const int col = nb * 16 + li;
     // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] 16-bit.  The
@@ -179,10 +208,13 @@ struct Band6Ops {
       bool live[MCH];
 #pragma unroll
       for (int j = 0; j < MCH; ++j) {
-        const int mb = mb0 + (chn * MCH + j) * G::WPN;
+        const int mb = L::TILE4 ? mb0 * G::MBW + j : mb0 + (chn * MCH + j) * G::WPN;
         const int row = mb * 16 + li;
         int oy, ox;
-        if constexpr (G::POOL) {
+        if constexpr (L::TILE4) {
+          oy = li >> 2;
+          ox = 4 * mb + (li & 3);
+        } else if constexpr (G::POOL) {
           const int w = row >> 2, sb = row & 3;
           const int ph = w / (G::WO / 2), pw = w - ph * (G::WO / 2);
           oy = 2 * ph + (sb >> 1);
@@ -228,7 +260,10 @@ struct Band6Ops {
         if constexpr (L::DBUF) read_a(0, avb[0]);
 #pragma unroll
         for (int t = 0; t < L::NT; ++t) {
-          if (t + LA < L::NT) {
+#ifndef BA3C_DIAG_NOB
+#define BA3C_DIAG_NOB 0       // diagnostics only: B fragments of the first k-steps reused
+#endif
+          if (!BA3C_DIAG_NOB && t + LA < L::NT) {
 #pragma unroll
             for (int s = 0; s < L::NS; ++s)
               bring[(t + LA) % (LA + 1)][s] = *reinterpret_cast<const uint4*>(wph + s * WSPLIT + koff(t + LA));
@@ -242,15 +277,29 @@ struct Band6Ops {
           u32x4 b[L::NS];
 #pragma unroll
           for (int s = 0; s < L::NS; ++s) {
-            const uint4 u = bring[t % (LA + 1)][s];
+            const uint4 u = bring[BA3C_DIAG_NOB ? t % LA : t % (LA + 1)][s];
             b[s] = u32x4{u.x, u.y, u.z, u.w};
           }
           // NS = 3: a1b1, a1b2, a2b1, a1b3, a2b2, a3b1;  NS = 2: a1b1, a1b2, a2b1 —
           // interleaved over m-blocks
+          auto mfmas = [&]() {
 #pragma unroll
-          for (int pr = 0; pr < SP::NPROD; ++pr)
+            for (int pr = 0; pr < SP::NPROD; ++pr)
 #pragma unroll
-            for (int j = 0; j < MCH; ++j) acc[j] = SP::mfma(avb[L::DBUF ? (t & 1) : 0][SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
+              for (int j = 0; j < MCH; ++j) {
+                if constexpr (L::TILE4) {
+                  // edge tile: tap column kw = 0 (left) / KW-1 (right) reads only padding
+                  const int kw = (t / L::K32) % G::KW;
+                  if ((MB0 == 0 && j == 0 && kw == 0) || (MB0 == 1 && j == MCH - 1 && kw == G::KW - 1)) continue;
+                }
+                acc[j] = SP::mfma(avb[L::DBUF ? (t & 1) : 0][SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
+              }
+          };
+          if constexpr (L::TILE4) {
+            if ((t / L::K32) / G::KW != kh_skip) mfmas();     // wave-uniform branch
+          } else {
+            mfmas();
+          }
         }
       }
 
@@ -258,7 +307,7 @@ struct Band6Ops {
       // un-scale by 2^-(ka + kw) (two exact power-of-two products)
 #pragma unroll
       for (int j = 0; j < MCH; ++j) {
-        const int mb = mb0 + (chn * MCH + j) * G::WPN;
+        const int mb = L::TILE4 ? mb0 * G::MBW + j : mb0 + (chn * MCH + j) * G::WPN;
         if (!live[j]) continue;
         if constexpr (G::POOL) {
           const int w = mb * 4 + lq;
@@ -281,7 +330,8 @@ struct Band6Ops {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = mb * 16 + lq * 4 + r;
-            const int oy = row / G::WO, ox = row - oy * G::WO;
+            // TILE4: accumulator row 4 lq + r of tile mb is pixel (lq, 4 mb + r)
+            const int oy = L::TILE4 ? lq : row / G::WO, ox = L::TILE4 ? 4 * mb + r : row - oy * G::WO;
             if (row < G::MROWS && oy < rows_out) {
               const float out = acc[j][r] * us1 * us2;
               omax = fmaxf(omax, fabsf(out));
@@ -357,6 +407,17 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
   float4 pv[PRE ? NNEW : 1];
   uint32_t pc[PRE ? NNEW : 1];
   unsigned long long pos = 0;
+#ifndef BA3C_STAGGER
+#define BA3C_STAGGER 0        // A/B: cycles (x64) the second workgroup of a CU sleeps at start
+#endif
+#ifndef BA3C_PRIO2
+#define BA3C_PRIO2 0          // A/B: the second workgroup of a CU runs at s_setprio 1
+#endif
+  if (BA3C_STAGGER && bx >= gx / 2) {
+    for (int i = 0; i < BA3C_STAGGER / 127; ++i) __builtin_amdgcn_s_sleep(127);
+    __builtin_amdgcn_s_sleep(BA3C_STAGGER % 127);
+  }
+  if (BA3C_PRIO2 && bx >= gx / 2) __builtin_amdgcn_s_setprio(1);
   for (int img = img0; img < img1; ++img) {
     const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
     const float asc = exp2i(ka), us1 = exp2i(-ka);
@@ -366,7 +427,15 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
       const int rows_out = min(G::RB, G::HO - y0);
       __syncthreads();                                      // previous band's LDS reads are done
       unsigned fbase = 0;
-      if (bi > 0) {
+#ifndef BA3C_DIAG_NOSTAGE
+#define BA3C_DIAG_NOSTAGE 0   // diagnostics only (A/B timing builds): skip the band staging
+#endif
+#ifndef BA3C_DIAG_NOCOMPUTE
+#define BA3C_DIAG_NOCOMPUTE 0 // diagnostics only: skip the MFMA main loop and epilogue
+#endif
+      if (BA3C_DIAG_NOSTAGE) {
+        __syncthreads();
+      } else if (bi > 0) {
         // carry the halo rows down: source rows RB .. SROWS-1 -> rows 0 .. HALO-1.  The new
         // rows then go to rows HALO .. SROWS-1, which overlap the source rows (RB >= HALO), and
         // a thread's copy elements are not the rows its stores write: every wave's copy must
@@ -379,7 +448,8 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
         fbase = FNEW;                                       // stage rows HALO .. SROWS-1 only
         __syncthreads();
       }
-      if (PRE && bi > 0) {
+      if (BA3C_DIAG_NOSTAGE) {
+      } else if (PRE && bi > 0) {
         // the new rows were prefetched during the previous band's MFMAs
 #pragma unroll
         for (int i = 0; i < NNEW; ++i) O::store1(lds, y0, rows_out, FNEW + tid + 256u * i, pv[i], pc[i], asc);
@@ -397,12 +467,12 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
         }
       }
       __syncthreads();
-      if (PRE && bi + 1 < G::NBANDS) {
+      if (PRE && !BA3C_DIAG_NOSTAGE && bi + 1 < G::NBANDS) {
         const int y1 = y0 + G::RB, ro1 = min(G::RB, G::HO - y1);
 #pragma unroll
         for (int i = 0; i < NNEW; ++i) O::load1(a, img, y1, ro1, 0, FNEW + tid + 256u * i, pv[i], pc[i]);
       }
-      O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [](int) {});
+      if (!BA3C_DIAG_NOCOMPUTE) O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [](int) {});
     }
     if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
   }

@@ -172,7 +172,14 @@ struct Lay<2> {
   using C1F = Band6<GConv1F, 160, 128, 7, 0, 2, true>;
   using C1FP = Band6<GConv1F, 160, 128, 7, 0, 2, false>;   // pipelined: no spill without DBUF
   using C2F = Band6<GConv2F, 160, 64, 7, 0, 2>;
+#ifndef BA3C_C1D_TILE4
+#define BA3C_C1D_TILE4 1
+#endif
+#if BA3C_C1D_TILE4
+  using C1D = Band6<GConv1D, 160, 0, 5, 0, 2, true, true>;   // 4x4 tiles: RP = 128 mod 256 B
+#else
   using C1D = Band6<GConv1D, 160, 128, 5, 0, 2, true>;
+#endif
   using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2>;
   using C2FS = Band6<GConv2FS, 160, 64, 2, 0, 2, true>;
   using C2DS = Band6<GConv2DS, 160, 128, 2, 32, 2, true>;

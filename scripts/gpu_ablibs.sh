@@ -14,5 +14,5 @@ for f in gpurun_out/$tag/bench_*.log; do
   echo "$f"; grep -h '^{' $f | python -c "
 import sys,json
 for l in sys.stdin:
-    d=json.loads(l); k=d['kernel_ms_one_step']; print(d['value'], d['ms_per_step'], {x: k[x] for x in ('conv0_fwd','conv0_wgrad','conv1_fwd','conv1_dgrad','conv1_wgrad')})"
+    d=json.loads(l); k=d['kernel_ms_one_step']; print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_launch_ms'], {x: k[x] for x in ('conv0_fwd','conv0_wgrad','conv1_fwd','conv1_dgrad','conv1_wgrad')})"
 done
