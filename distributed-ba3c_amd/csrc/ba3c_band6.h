@@ -191,15 +191,22 @@ struct Band6Ops {
     const int kh_skip = !L::TILE4 ? -1 : (y0 == 0 ? 0 : (y0 + G::RB == G::HO ? G::KH - 1 : -1));
     const int li = lane & 15, lq = lane >> 4;
     const int col = nb * 16 + li;
-    // B: lane reads n = col, k = 32 t + 8 lq of split s: [s][COUT][KDIM] 16-bit.  The
-    // offset goes through an empty asm so a persistent caller's band loop cannot hoist the
-    // (band-invariant) weight loads of all k-steps out of the loop into registers.
-    int woff = col * G::KDIM + 8 * lq;
+    // B: lane reads n = col, k = 32 t + 8 lq of split s, stored in MFMA fragment order
+    // [s][K / 32][COUT / 16][lane] x 16 B (wprep6_body), so one wave's fragment is 1 KB
+    // contiguous.  The offset goes through an empty asm so a persistent caller's band loop
+    // cannot hoist the (band-invariant) weight loads of all k-steps out of the loop into
+    // registers.
+#ifndef BA3C_WFRAG
+#define BA3C_WFRAG 1          // 0: A/B build with the plain [s][COUT][KDIM] weight order
+#endif
+    int woff = BA3C_WFRAG ? nb * 512 + lane * 8 : col * G::KDIM + 8 * lq;
     asm volatile("" : "+v"(woff));
     const uint16_t* wrow = a.wt6 + woff;
     constexpr size_t WSPLIT = (size_t)G::COUT * G::KDIM;
+    // fragment offset (16-bit units) of K index k0 (a multiple of 32)
+    auto kfrag = [](int k0) { return BA3C_WFRAG ? (k0 / 32) * G::NB * 512 : k0; };
     // K index (tap, channel) of k-step t of a phase, relative to the phase's first channel
-    auto koff = [](int t) { return (t / L::K32) * G::CIN + (t % L::K32) * 32; };
+    auto koff = [&](int t) { return kfrag((t / L::K32) * G::CIN + (t % L::K32) * 32); };
 
 #pragma unroll
     for (int chn = 0; chn < L::NCH; ++chn) {
@@ -234,7 +241,7 @@ struct Band6Ops {
 #pragma unroll 1
       for (int ph = 0; ph < L::NPH; ++ph) {
         if constexpr (L::NPH > 1) stage_phase(ph);
-        const uint16_t* wph = wrow + ph * L::KPH;
+        const uint16_t* wph = wrow + kfrag(ph * L::KPH);
         constexpr int LA = 3;
         uint4 bring[LA + 1][L::NS];
 #pragma unroll
@@ -602,19 +609,26 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
     sc = exp2i(k);
   }
   uint16_t* dst = a.wt6 + NS * (size_t)a.off[y];
-  for (int e = bx * 256 + threadIdx.x; e < j.n; e += gx * 256) {
+  // destination d in the band kernels' MFMA B-fragment order [K / 32][N / 16][lane][8]: lane
+  // (lq, li) holds column n = 16 nb + li, K = 32 k32 + 8 lq .. + 7 (Band6Ops::compute)
+  const int K = j.KH * j.KW * (j.dgrad ? j.CO : j.CI);
+  const int NB = j.n / K / 16;
+  for (int d = bx * 256 + threadIdx.x; d < j.n; d += gx * 256) {
+    const int kk = d & 7, li = (d >> 3) & 15, lq = (d >> 7) & 3, rest = d >> 9;
+    const int k32 = rest / NB, nb = rest - k32 * NB;
+    const int e = BA3C_WFRAG ? (nb * 16 + li) * K + k32 * 32 + lq * 8 + kk : d;
     const float v = wprep_value(j, e);
     if constexpr (NS == 3) {
       uint32_t hi, mid, lo;
       split3(v, hi, mid, lo);
-      dst[e] = (uint16_t)hi;
-      dst[j.n + e] = (uint16_t)mid;
-      dst[2 * j.n + e] = (uint16_t)lo;
+      dst[d] = (uint16_t)hi;
+      dst[j.n + d] = (uint16_t)mid;
+      dst[2 * j.n + d] = (uint16_t)lo;
     } else {
       uint32_t hi, lo;
       split2(v * sc, hi, lo);
-      dst[e] = (uint16_t)hi;
-      dst[j.n + e] = (uint16_t)lo;
+      dst[d] = (uint16_t)hi;
+      dst[j.n + d] = (uint16_t)lo;
     }
   }
 }
