@@ -75,6 +75,8 @@ struct ba3c_handle {
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  bool w6w = true;    // conv1 weight gradient, B >= W6W_MIN_B: all channels per workgroup
+                      // (BA3C_W6W=0: two 16-channel groups, wgrad6_kernel)
   // conv1 fwd / dgrad on the pipelined persistent band kernel (BA3C_PIPE=1).  Off: r02e
   // measured it slower (conv1 fwd 0.41 -> 0.51 ms, dgrad 0.43 -> 0.47 ms) — one compute wave
   // per SIMD exposes the LDS-read latency that two co-resident one-band workgroups hide.
@@ -185,6 +187,7 @@ struct Lay<2> {
   using C2DS = Band6<GConv2DS, 160, 128, 2, 32, 2, true>;
   using W1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 160, 2>;
   using W2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 160, 2>;
+  using W1W = Wg6WGeom<40, 40, 32, 32, 4, 160, 160>;   // conv1, B >= W6W_MIN_B (76.8 KB LDS)
 };
 // weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
 using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
@@ -196,6 +199,10 @@ constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workg
 // workgroup made 256 partial slabs of 100 KB — 26 MB written and read back by the reduction
 // for 3.3 MB of input).  A function of B alone, so every launch path sums the same slabs.
 inline int conv1_wgrad_p(int B) { return std::max(64, std::min(W6_P1, B * 9 / 4)); }
+// conv1 weight gradient with all 32 input channels per workgroup (wgrad6w_kernel) from this
+// batch on: whole images per workgroup, two workgroups per CU, one slab each
+constexpr int W6W_MIN_B = 512, W6W_P = 512;
+static_assert(W6W_P <= WG_P1, "conv1 partial slabs: the allocation covers WG_P1 slabs");
 constexpr int FW_P0S = 512;   // conv0s_fwd_kernel: persistent, two workgroups per CU
 constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
@@ -952,7 +959,23 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
         s, da, dim3(B * LY::C1D::G::NBANDS), wa, wg)));
     CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[1]].offset));
   } else {
-    if (h->band && h->w6) {
+    bool done = false;
+    if constexpr (NS == 2) {
+      if (h->band && h->w6 && h->w6w && B >= W6W_MIN_B) {
+        using GW = typename LY::W1W;
+        const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
+        const int P = std::min(W6W_P, B);
+        {
+          ProbeScope ps(h, ws, BA3C_K_CONV1_WGRAD);
+          hipLaunchKernelGGL(wgrad6w_kernel<GW>, dim3(P), dim3(256), 0, ws, wa);
+        }
+        HIP_TRY(hipGetLastError());
+        CHECK(reduce_wgrad6<typename LY::W1>(h, ws, wa, P, grads + h->tensors[h->idx_conv[1]].offset));
+        done = true;
+      }
+    }
+    if (done) {
+    } else if (h->band && h->w6) {
       CHECK(launch_wgrad6<typename LY::W1>(h, ws, BA3C_K_CONV1_WGRAD,
                                           Wg6Args{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)},
                                           conv1_wgrad_p(B), grads + h->tensors[h->idx_conv[1]].offset));
@@ -1088,6 +1111,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
+  if (const char* e = getenv("BA3C_W6W")) h->w6w = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
   if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
   if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 3;

@@ -214,13 +214,19 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
     const int kvalid = rows_out * G::WO;
     // first window row of this band in the X slots (ring: slot bi & 1)
     const int xbase = ring ? (bi & 1) * G::RB * G::WS * G::PX : 0;
+#ifndef BA3C_DIAG_W6
+#define BA3C_DIAG_W6 0        // diagnostics only (A/B timing): 1 = no staging, 2 = no MFMA loop
+#endif
     __syncthreads();                                      // previous band's LDS reads done
-    store_band(band);
+    if (BA3C_DIAG_W6 != 1) store_band(band);
     __syncthreads();
-    if (band + bstep < band_end) load_band(band + bstep);
+    if (BA3C_DIAG_W6 != 1 && band + bstep < band_end) load_band(band + bstep);
 
-#pragma unroll 1
-    for (int s = 0; s < G::KS; ++s) {
+#ifndef BA3C_W6_UNROLL
+#define BA3C_W6_UNROLL 1      // k-steps unrolled per loop iteration (A/B)
+#endif
+#pragma unroll BA3C_W6_UNROLL
+    for (int s = 0; s < (BA3C_DIAG_W6 == 2 ? 0 : G::KS); ++s) {
       // this lane's pixel rows for tr reads r = 0, 1
       int xb[2], yb[2];
 #pragma unroll
@@ -240,19 +246,34 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
           const uint2 u1 = lds_tr16(ys + yb[1] + nb * 32 + sp * G::YSB);
           b[nb][sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
         }
-#pragma unroll
-      for (int t = 0; t < G::TW; ++t) {
-        if (t >= ntap) break;
+      // A fragments of tap t + 1 are read into the second register set before tap t's MFMAs
+      // (one set made every tap wait a full LDS round trip before its MFMAs)
+      auto read_a = [&](int t, u32x4 (&av)[G::NS]) {
         const int tap = tap0 + t;
         const int kh = tap / G::KW, kw = tap - kh * G::KW;
         const int toff = (kh * G::WS + kw) * G::PX;
-        u32x4 av[G::NS];
 #pragma unroll
         for (int sp = 0; sp < G::NS; ++sp) {
           const uint2 u0 = lds_tr16(xs + xb[0] + toff + sp * G::XSB);
           const uint2 u1 = lds_tr16(xs + xb[1] + toff + sp * G::XSB);
           av[sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
         }
+      };
+#ifndef BA3C_W6_DBUF
+#define BA3C_W6_DBUF 1
+#endif
+      u32x4 avb[2][G::NS];
+      if (BA3C_W6_DBUF) read_a(0, avb[0]);
+#pragma unroll
+      for (int t = 0; t < G::TW; ++t) {
+        if (t >= ntap) break;
+        if (BA3C_W6_DBUF) {
+          if (t + 1 < ntap) read_a(t + 1, avb[(t + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);              // keep those reads ahead of the MFMAs
+        } else {
+          read_a(t, avb[t & 1]);
+        }
+        const u32x4 (&av)[G::NS] = avb[t & 1];
         // the family's cross products, interleaved over the two n-blocks
 #pragma unroll
         for (int pr = 0; pr < SP::NPROD; ++pr)
@@ -280,6 +301,235 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Whole-channel variant (conv1 at large batches, scaled fp16 family).  wgrad6_body gives each
+// workgroup 16 of the 32 input channels, so the un-pooled, split dY of every band was loaded and
+// split twice (once per channel group: r02 PMC 978 MB per launch against 550 MB algorithmic).
+// Here one workgroup takes all (tap, c) rows of its images: dY is staged once, X (all 32
+// channels) lives in an XROWS-row window — band i + 1's first HALO rows are band i's last ones
+// and move down with one LDS-to-LDS copy, so only RB new rows are loaded and split — and the
+// workgroup writes one full [M][COUT] partial slab.  Wave w owns a run of 7 / 6 / 6 / 6 taps x
+// both 16-channel c-blocks x both 16-column n-blocks.  Per output the accumulation runs over
+// the same k-steps in the same order as wgrad6_body's (bands in order, 32 permuted pixels per
+// k-step); only the grouping of images into slabs differs.
+template <int HS_, int WS_, int CIN_, int COUT_, int RB_, int PX_, int PY_>
+struct Wg6WGeom {
+  static constexpr int NS = 2;
+  static constexpr int HS = HS_, WS = WS_, CIN = CIN_, COUT = COUT_, RB = RB_;
+  static constexpr int KH = 5, KW = 5, NTAP = 25;
+  static constexpr int HO = HS - KH + 1, WO = WS - KW + 1, PH = HO / 2, PW = WO / 2;
+  static constexpr int NBANDS = HO / RB;
+  static constexpr int KP = RB * WO, KS = (KP + 31) / 32, KPAD = 32 * KS;
+  static constexpr int HALO = KH - 1, XROWS = RB + HALO;
+  static constexpr int PX = PX_, PY = PY_;
+  static constexpr int XSB = 2 * CIN, YSB = 2 * COUT;
+  static constexpr int X_BYTES = XROWS * WS * PX, Y_BYTES = KPAD * PY;
+  static constexpr int CB = CIN / 16, NB = COUT / 16;
+  static constexpr int TBASE = NTAP / 4, TREM = NTAP % 4, TW = TBASE + (TREM > 0);
+  static constexpr int M = NTAP * CIN;
+  static_assert(HO % RB == 0 && RB == HALO, "whole bands; the halo copy's ranges are disjoint");
+  static_assert(PX >= NS * XSB && PY >= NS * YSB && PX % 32 == 0 && PY % 32 == 0, "pitches");
+  static_assert(RB * WS * (CIN / 4) % 256 == 0, "new X rows: whole float4 per thread");
+  static_assert(X_BYTES % 16 == 0 && (HALO * WS * PX) % 16 == 0, "wgrad6w geometry");
+};
+
+template <class G>
+__device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
+  using SP = SplitP<G::NS>;
+  const int kx = amax_exp(amax_all(a.amax_x, a.batch, red4));
+  const int ky = amax_exp(amax_all(a.amax_dp, a.batch, red4));
+  const float xsc = exp2i(kx), ysc = exp2i(ky);
+  char* ys = xs + G::X_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tap0 = wave * G::TBASE + min(wave, G::TREM);
+  const int ntap = G::TBASE + (wave < G::TREM);
+  const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+  const int kperm = 16 * (g >> 1) + 4 * (g & 1) + q;      // + 8 r for read r (wgrad6_body)
+
+  f32x4 acc[G::TW][G::CB][G::NB];
+#pragma unroll
+  for (int t = 0; t < G::TW; ++t)
+#pragma unroll
+    for (int cb = 0; cb < G::CB; ++cb)
+#pragma unroll
+      for (int nb = 0; nb < G::NB; ++nb) acc[t][cb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int XQ = G::CIN / 4;                          // float4 per X pixel
+  constexpr int XPT = G::RB * G::WS * XQ / 256;           // float4 of RB rows per thread
+  constexpr int YQ = G::COUT / 4;
+  constexpr int YN = G::KPAD * YQ;
+  constexpr int YPT = (YN + 255) / 256;
+  float4 xv[XPT], yv[YPT];
+  uint32_t yc[YPT];
+
+  const int ipw = (a.batch + gx - 1) / gx;                // whole images per workgroup
+  const int img0 = min(a.batch, bx * ipw), img1 = min(a.batch, img0 + ipw);
+  const int band_end = img1 * G::NBANDS;
+
+  // RB image rows from row y of image img -> registers
+  auto load_x = [&](int img, int y, float4 (&v)[XPT]) {
+    const float* src = a.x + ((size_t)(img * G::HS + y) * G::WS) * G::CIN;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) v[i] = reinterpret_cast<const float4*>(src)[tid + 256 * i];
+  };
+  auto load_y = [&](int img, int bi) {
+    const int y0 = bi * G::RB;
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + 256 * i;
+      const int p = f / YQ, oq = f - p * YQ;
+      const int ry = p / G::WO, x = p - ry * G::WO;
+      yv[i] = f4zero();
+      yc[i] = 0;
+      if (f < YN && ry < G::RB) {
+        const int y = y0 + ry;
+        const size_t pidx = (size_t)(img * G::PH + (y >> 1)) * G::PW + (x >> 1);
+        yv[i] = *reinterpret_cast<const float4*>(a.dp + pidx * G::COUT + oq * 4);
+        yc[i] = *reinterpret_cast<const uint32_t*>(a.code + pidx * G::COUT + oq * 4);
+      }
+    }
+  };
+  // RB rows -> window rows wr .. wr + RB - 1, split
+  auto store_x = [&](int wr, const float4 (&v)[XPT]) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int f = tid + 256 * i;
+      const int pix = f / XQ, cq = f - pix * XQ;
+      uint32_t s0[G::NS], s1[G::NS];
+      SP::split(v[i].x, v[i].y, xsc, s0);
+      SP::split(v[i].z, v[i].w, xsc, s1);
+      char* p = xs + (wr * G::WS + pix) * G::PX + cq * 8;
+#pragma unroll
+      for (int sp = 0; sp < G::NS; ++sp) *reinterpret_cast<uint2*>(p + sp * G::XSB) = make_uint2(s0[sp], s1[sp]);
+    }
+  };
+  auto store_y = [&](int bi) {
+    const int y0 = bi * G::RB;
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + 256 * i;
+      if (f < YN) {
+        const int p = f / YQ, oq = f - p * YQ;
+        const int ry = p / G::WO, x = p - ry * G::WO;
+        const uint32_t sb = (((y0 + ry) & 1) << 1) | (x & 1), c = yc[i];
+        float e[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = ((c >> (8 * k)) & 255u) == sb ? e[k] : 0.f;
+        uint32_t s0[G::NS], s1[G::NS];
+        SP::split(e[0], e[1], ysc, s0);
+        SP::split(e[2], e[3], ysc, s1);
+        char* d = ys + p * G::PY + oq * 8;
+#pragma unroll
+        for (int sp = 0; sp < G::NS; ++sp) *reinterpret_cast<uint2*>(d + sp * G::YSB) = make_uint2(s0[sp], s1[sp]);
+      }
+    }
+  };
+
+  int band = img0 * G::NBANDS;
+  if (band < band_end) {
+    load_x(img0, G::HALO, xv);
+    load_y(img0, 0);
+  }
+  for (; band < band_end; ++band) {
+    const int img = band / G::NBANDS;
+    const int bi = band - img * G::NBANDS;
+    __syncthreads();                                      // previous band's LDS reads are done
+    if (bi > 0) {
+      // window rows RB .. RB + HALO - 1 -> 0 .. HALO - 1 (disjoint); every wave's copy is
+      // complete before any wave stores the new rows over the source rows (barrier)
+      constexpr int N16 = G::HALO * G::WS * G::PX / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(xs + G::RB * G::WS * G::PX);
+      uint4* dst = reinterpret_cast<uint4*>(xs);
+      for (int i = tid; i < N16; i += 256) dst[i] = src[i];
+      __syncthreads();
+    }
+    store_x(G::HALO, xv);
+    store_y(bi);
+    if (bi == 0) {                                        // an image's first HALO rows
+      load_x(img, 0, xv);
+      store_x(0, xv);
+    }
+    __syncthreads();
+    if (band + 1 < band_end) {
+      const int ni = (band + 1) / G::NBANDS, nbi = band + 1 - ni * G::NBANDS;
+      load_x(ni, nbi * G::RB + G::HALO, xv);
+      load_y(ni, nbi);
+    }
+#pragma unroll 1
+    for (int s = 0; s < G::KS; ++s) {
+      int xb[2], yb[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        int p = 32 * s + kperm + 8 * r;
+        yb[r] = p * G::PY + 8 * pq;
+        if (p >= G::KP) p = 0;                            // padded pixels: dY is zero
+        const int y = p / G::WO, x = p - y * G::WO;
+        xb[r] = (y * G::WS + x) * G::PX + 8 * pq;
+      }
+      u32x4 b[G::NB][G::NS];
+#pragma unroll
+      for (int nb = 0; nb < G::NB; ++nb)
+#pragma unroll
+        for (int sp = 0; sp < G::NS; ++sp) {
+          const uint2 u0 = lds_tr16(ys + yb[0] + nb * 32 + sp * G::YSB);
+          const uint2 u1 = lds_tr16(ys + yb[1] + nb * 32 + sp * G::YSB);
+          b[nb][sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
+        }
+#pragma unroll
+      for (int t = 0; t < G::TW; ++t) {
+        if (t >= ntap) break;
+        const int tap = tap0 + t;
+        const int kh = tap / G::KW, kw = tap - kh * G::KW;
+        const int toff = (kh * G::WS + kw) * G::PX;
+        u32x4 av[G::CB][G::NS];
+#pragma unroll
+        for (int cb = 0; cb < G::CB; ++cb)
+#pragma unroll
+          for (int sp = 0; sp < G::NS; ++sp) {
+            const uint2 u0 = lds_tr16(xs + xb[0] + toff + sp * G::XSB + cb * 32);
+            const uint2 u1 = lds_tr16(xs + xb[1] + toff + sp * G::XSB + cb * 32);
+            av[cb][sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
+          }
+#pragma unroll
+        for (int pr = 0; pr < SP::NPROD; ++pr)
+#pragma unroll
+          for (int cb = 0; cb < G::CB; ++cb)
+#pragma unroll
+            for (int nb = 0; nb < G::NB; ++nb)
+              acc[t][cb][nb] = SP::mfma(av[cb][SP::pa(pr)], b[nb][SP::pb(pr)], acc[t][cb][nb]);
+      }
+    }
+  }
+
+  // ---- epilogue: one full slab per workgroup (lane: column o = 16 nb + (lane & 15), rows
+  // c = 16 cb + 4 (lane >> 4) + r) ----
+  float* pz = a.part + (size_t)bx * G::M * G::COUT;
+  const float us1 = exp2i(-kx), us2 = exp2i(-ky);
+#pragma unroll
+  for (int t = 0; t < G::TW; ++t) {
+    if (t >= ntap) break;
+    const int tap = tap0 + t;
+#pragma unroll
+    for (int cb = 0; cb < G::CB; ++cb)
+#pragma unroll
+      for (int nb = 0; nb < G::NB; ++nb) {
+        const int o = nb * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb * 16 + 4 * (lane >> 4) + r;
+          pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[t][cb][nb][r] * us1 * us2;
+        }
+      }
+  }
+}
+
+template <class G>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wgrad6w_kernel(const Wg6Args a) {
+  __shared__ uint4 lds4[(G::X_BYTES + G::Y_BYTES) / 16];
+  __shared__ uint32_t red4[4];
+  wgrad6w_body<G>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4), red4);
 }
 
 template <class G>

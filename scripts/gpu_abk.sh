@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of one kernel over library builds, alternating A B .. A B twice:
-#   scripts/gpu_abk.sh TAG KERNEL default|lib1.so lib2.so ...
+#   scripts/gpu_abk.sh TAG KERNEL default|lib1.so|ENV=VAL ...
 # each run times KERNEL over the 30 timed steps (BA3C_BENCH_PROBE) and prints its average
 # launch time and the step throughput.
 set -o pipefail
@@ -10,7 +10,9 @@ S=scripts/gpu_step.sh
 for rep in 1 2; do
   for lib in "$@"; do
     n=$(basename $lib .so)
-    if [ "$lib" = default ]; then ev=(); else ev=(BA3C_LIB=$lib); fi
+    if [ "$lib" = default ]; then ev=();
+    elif [[ "$lib" == *=* ]]; then ev=($lib); n=$(echo $lib | tr '=' '_');   # an env setting
+    else ev=(BA3C_LIB=$lib); fi
     $S 300 gpurun_out/$tag/bench_${n}_$rep.log env "${ev[@]}" BA3C_BENCH_PROBE=$k python bench.py --no-cpu-baseline --no-overlap --no-b32 || exit $?
   done
 done
