@@ -34,7 +34,7 @@ namespace ba3c {
 // footprint => more workgroups per CU to hide the staging); accumulators persist across
 // phases, so a phased layout needs all of a wave's m-blocks in one chunk.
 template <class G_, int PP_, int RPX_, int MCH_, int KPH_ = 0, int NS_ = 3, bool DBUF_ = false,
-          bool TILE4_ = false>
+          bool TILE4_ = false, bool PADSKIP_ = false>
 struct Band6 {
   // DBUF: A fragments of k-step t + 1 read into a second register set before k-step t's
   // MFMAs (only where the registers allow it without spilling)
@@ -47,7 +47,18 @@ struct Band6 {
   // band.  Those MFMAs multiply exact zeros and are not issued (8 % of conv1's input-gradient
   // MFMAs); an MFMA adds its products to the accumulator exactly, so nothing else changes.
   static constexpr bool TILE4 = TILE4_;
+  // PADSKIP (input-gradient layouts whose one band is the whole map): an m-block of 16
+  // consecutive pixels spans one or two output rows; tap rows kh that read only the zero
+  // padding for all of them are not issued.  The band is fixed, so the skipped (m-block, tap)
+  // pairs are compile-time (conv2: 22 % of the MFMAs, the same count for both waves of an
+  // n-block).
+  static constexpr bool PADSKIP = PADSKIP_;
   using G = G_;
+  __host__ __device__ static constexpr bool pad_kh(int mb, int kh) {
+    return 16 * mb >= G_::MROWS ||
+           kh < G_::PADY - (16 * mb + 15 < G_::MROWS ? 16 * mb + 15 : G_::MROWS - 1) / G_::WO ||
+           kh > G_::PADY - (16 * mb) / G_::WO + G_::UHO - 1;
+  }
   static constexpr int NS = NS_;                         // split planes (3 bf16 / 2 fp16)
   static constexpr int KPH = KPH_ ? KPH_ : G_::CIN;
   static constexpr int NPH = G_::CIN / KPH;
@@ -67,6 +78,9 @@ struct Band6 {
                            G::PADY == G::KH - 1 && G::UWO + 2 * G::PADX == G::WS &&
                            G::UHO + 2 * G::PADY == G::HS),
                 "4x4 tiles: input-gradient bands of 4 rows, one m-block chunk per wave");
+  static_assert(!PADSKIP || (!TILE4 && !G::POOL && G::SRC == 1 && G::NBANDS == 1 && G::WPN == 2 &&
+                             NCH == 1 && G::UHO + 2 * G::PADY == G::HS),
+                "padding skip: one whole-map band, one m-block chunk per wave");
 };
 
 struct Band6Args {
@@ -170,8 +184,9 @@ struct Band6Ops {
   __device__ static void compute(const Band6Args& a, const char* lds, int wave, int lane, int img, int y0,
                                  int rows_out, float us1, float us2, unsigned long long& pos, float& omax,
                                  StageFn&& stage_phase) {
-    if constexpr (L::TILE4) {
-      // the wave's edge tile (left for waves of tiles 0..4, right for 5..9) is compile-time
+    if constexpr (L::TILE4 || L::PADSKIP) {
+      // TILE4: the wave's edge tile (left for waves of tiles 0..4, right for 5..9) and PADSKIP:
+      // the wave's m-blocks are compile-time
       if (wave / G::NB == 0) compute_t<0>(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, stage_phase);
       else compute_t<1>(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, stage_phase);
     } else {
@@ -186,7 +201,7 @@ struct Band6Ops {
     // instead of being hoisted out of a persistent caller's band loop into live registers
     asm volatile("" : "+v"(lane));
     const int nb = wave % G::NB;
-    const int mb0 = L::TILE4 ? MB0 : wave / G::NB;
+    const int mb0 = (L::TILE4 || L::PADSKIP) ? MB0 : wave / G::NB;
     // TILE4: tap row kh_skip reads only padding for every tile of this band (-1: none)
     const int kh_skip = !L::TILE4 ? -1 : (y0 == 0 ? 0 : (y0 + G::RB == G::HO ? G::KH - 1 : -1));
     const int li = lane & 15, lq = lane >> 4;
@@ -298,6 +313,9 @@ struct Band6Ops {
                   // edge tile: tap column kw = 0 (left) / KW-1 (right) reads only padding
                   const int kw = (t / L::K32) % G::KW;
                   if ((MB0 == 0 && j == 0 && kw == 0) || (MB0 == 1 && j == MCH - 1 && kw == G::KW - 1)) continue;
+                }
+                if constexpr (L::PADSKIP) {
+                  if (L::pad_kh(MB0 + j * G::WPN, (t / L::K32) / G::KW)) continue;
                 }
                 acc[j] = SP::mfma(avb[L::DBUF ? (t & 1) : 0][SP::pa(pr)][j], b[SP::pb(pr)], acc[j]);
               }

@@ -182,7 +182,10 @@ struct Lay<2> {
 #else
   using C1D = Band6<GConv1D, 160, 128, 5, 0, 2, true>;
 #endif
-  using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2>;
+#ifndef BA3C_C2D_PADSKIP
+#define BA3C_C2D_PADSKIP 1
+#endif
+  using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2, false, false, BA3C_C2D_PADSKIP>;
   using C2FS = Band6<GConv2FS, 160, 64, 2, 0, 2, true>;
   using C2DS = Band6<GConv2DS, 160, 128, 2, 32, 2, true>;
   using W1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 160, 2>;
