@@ -432,17 +432,6 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
   float4 pv[PRE ? NNEW : 1];
   uint32_t pc[PRE ? NNEW : 1];
   unsigned long long pos = 0;
-#ifndef BA3C_STAGGER
-#define BA3C_STAGGER 0        // A/B: cycles (x64) the second workgroup of a CU sleeps at start
-#endif
-#ifndef BA3C_PRIO2
-#define BA3C_PRIO2 0          // A/B: the second workgroup of a CU runs at s_setprio 1
-#endif
-  if (BA3C_STAGGER && bx >= gx / 2) {
-    for (int i = 0; i < BA3C_STAGGER / 127; ++i) __builtin_amdgcn_s_sleep(127);
-    __builtin_amdgcn_s_sleep(BA3C_STAGGER % 127);
-  }
-  if (BA3C_PRIO2 && bx >= gx / 2) __builtin_amdgcn_s_setprio(1);
   for (int img = img0; img < img1; ++img) {
     const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
     const float asc = exp2i(ka), us1 = exp2i(-ka);
@@ -504,10 +493,134 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
   if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
 
+// zero-padded un-pooled dY staged from the POOLED map (ring walk of an input-gradient layout,
+// scaled fp16 family).  Band6Ops::store1 builds every staged float4 from the pooled float4 of
+// its 2x2 window: four global loads and four splits per pooled element, three of them splits
+// of zeros.  Here each (pooled pixel, 4 channels) is loaded and split ONCE and written to the
+// four pixels of its window with per-channel masks (code == position, compared as packed
+// 16-bit halves); the padding columns are zeroed once per workgroup and never written again,
+// padding rows are written as zeros.  Split values of zero are +0 either way, so the staged LDS
+// image is bit for bit the one store1 builds.
+__device__ __forceinline__ uint32_t mask16_eq0(uint32_t d) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  u16x2 x = __builtin_bit_cast(u16x2, d);
+  x = __builtin_elementwise_min(x, (u16x2){1, 1});   // 0 where the half matched, else 1
+  x = x + (u16x2){0xFFFF, 0xFFFF};                    // 0xFFFF where matched, else 0
+  return __builtin_bit_cast(uint32_t, x);
+}
+
+template <class L>
+__device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int gx, char* lds) {
+  using O = Band6Ops<L>;
+  using G = typename L::G;
+  using SP = SplitP<L::NS>;
+  constexpr int HALO = G::SROWS - G::RB;
+  static_assert(L::NS == 2 && G::SRC == 1 && L::NPH == 1 && !G::POOL && G::PADY == HALO &&
+                G::RB % 2 == 0 && G::UHO == 2 * G::UPH && G::UWO == 2 * G::UPW &&
+                G::UWO + 2 * G::PADX == G::WS && G::HO % G::RB == 0,
+                "pooled staging: padded input-gradient rings with whole windows per band");
+  constexpr int Q = O::Q;                                   // float4 per pixel
+  constexpr int NPI = (G::RB / 2) * G::UPW * Q;             // pooled items of the new rows
+  constexpr int IT = (NPI + 255) / 256;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float us2 = exp2i(-a.wexp[0]);
+  const int ipw = (a.batch + gx - 1) / gx;
+  const int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
+
+  // pooled rows bi * RB / 2 .. of image img (new rows of band bi: un-pooled rows y0 .. y0 +
+  // RB - 1 = staged rows HALO ..); rows past the map load as zero (value and code 0: the
+  // masked writes then store zeros)
+  auto load_items = [&](int img, int bi, float4 (&v)[IT], uint32_t (&c)[IT]) {
+    const int py0 = bi * (G::RB / 2);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int f = tid + 256 * i;
+      v[i] = f4zero();
+      c[i] = 0;
+      const int cq = f % Q, rest = f / Q;
+      const int pc = rest % G::UPW, py = py0 + rest / G::UPW;
+      if (f < NPI && py < G::UPH) {
+        const size_t off = ((size_t)(img * G::UPH + py) * G::UPW + pc) * G::CIN + cq * 4;
+        v[i] = *reinterpret_cast<const float4*>(a.src + off);
+        c[i] = *reinterpret_cast<const uint32_t*>(a.code + off);
+      }
+    }
+  };
+  auto store_items = [&](const float4 (&v)[IT], const uint32_t (&c)[IT], float asc) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int f = tid + 256 * i;
+      if (f < NPI) {
+        const int cq = f % Q, rest = f / Q;
+        const int pc = rest % G::UPW, pr = rest / G::UPW;
+        uint32_t s0[2], s1[2];
+        SP::split(v[i].x, v[i].y, asc, s0);
+        SP::split(v[i].z, v[i].w, asc, s1);
+        const uint32_t c01 = __builtin_amdgcn_perm(c[i], c[i], 0x0C010C00u);   // codes as halves
+        const uint32_t c23 = __builtin_amdgcn_perm(c[i], c[i], 0x0C030C02u);
+        char* base = lds + (HALO + 2 * pr) * L::RP + (G::PADX + 2 * pc) * L::PP + cq * 8;
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub) {
+          const uint32_t S = (uint32_t)sub * 0x00010001u;
+          const uint32_t m01 = mask16_eq0(c01 ^ S), m23 = mask16_eq0(c23 ^ S);
+          char* p = base + (sub >> 1) * L::RP + (sub & 1) * L::PP;
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp)
+            *reinterpret_cast<uint2*>(p + sp * L::SPB) = make_uint2(s0[sp] & m01, s1[sp] & m23);
+        }
+      }
+    }
+  };
+
+  // the whole band image starts zero: the padding columns are never written again
+  for (int i = tid; i < L::LDS_BYTES / 16; i += 256) reinterpret_cast<uint4*>(lds)[i] = make_uint4(0, 0, 0, 0);
+  float4 pv[IT];
+  uint32_t pc[IT];
+  if (img0 < img1) load_items(img0, 0, pv, pc);
+  unsigned long long pos = 0;
+  for (int img = img0; img < img1; ++img) {
+    const int ka = amax_exp(a.amax_in[1 + img]);            // per-image operand scale
+    const float asc = exp2i(ka), us1 = exp2i(-ka);
+    float omax = 0.f;
+    for (int bi = 0; bi < G::NBANDS; ++bi) {
+      const int y0 = bi * G::RB;
+      __syncthreads();                                      // previous band's LDS reads are done
+      if (bi > 0) {
+        // halo rows RB .. SROWS-1 -> 0 .. HALO-1; every wave's copy completes before any wave
+        // stores new rows over the source rows
+        constexpr int N16 = HALO * L::RP / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(lds + G::RB * L::RP);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (int i = tid; i < N16; i += 256) dst[i] = src[i];
+        __syncthreads();
+      } else {
+        // the first band's rows 0 .. HALO-1 are top padding
+        for (int i = tid; i < HALO * L::RP / 16; i += 256) reinterpret_cast<uint4*>(lds)[i] = make_uint4(0, 0, 0, 0);
+      }
+      store_items(pv, pc, asc);
+      __syncthreads();
+      {
+        // prefetch the workgroup's next band (the next image's first band after the last)
+        const int nb = bi + 1 < G::NBANDS ? bi + 1 : 0;
+        const int ni = bi + 1 < G::NBANDS ? img : img + 1;
+        if (ni < img1) load_items(ni, nb, pv, pc);
+      }
+      O::compute(a, lds, wave, lane, img, y0, G::RB, us1, us2, pos, omax, [](int) {});
+    }
+    amax_publish(a.amax_out, img, omax, lane);
+  }
+}
+
+#ifndef BA3C_UNPOOL_STAGE
+#define BA3C_UNPOOL_STAGE 1   // 0: A/B build with the per-pixel staging (Band6Ops::store1)
+#endif
 template <class L, bool PRE_ = L::G::SRC == 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6r_kernel(const Band6Args a) {
   __shared__ uint4 lds4[L::LDS_BYTES / 16];
-  band6r_body<L, PRE_>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
+  if constexpr (BA3C_UNPOOL_STAGE && L::G::SRC == 1 && L::NS == 2)
+    band6r_up_body<L>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
+  else
+    band6r_body<L, PRE_>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
 }
 
 // Pipelined persistent variant (NPH == 1 layouts): one 512-thread workgroup per CU walks

@@ -314,6 +314,15 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
 // both 16-channel c-blocks x both 16-column n-blocks.  Per output the accumulation runs over
 // the same k-steps in the same order as wgrad6_body's (bands in order, 32 permuted pixels per
 // k-step); only the grouping of images into slabs differs.
+// packed 16-bit halves: 0xFFFF where the half is zero, else 0
+__device__ __forceinline__ uint32_t w6_mask16_eq0(uint32_t d) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  u16x2 x = __builtin_bit_cast(u16x2, d);
+  x = __builtin_elementwise_min(x, (u16x2){1, 1});
+  x = x + (u16x2){0xFFFF, 0xFFFF};
+  return __builtin_bit_cast(uint32_t, x);
+}
+
 template <int HS_, int WS_, int CIN_, int COUT_, int RB_, int PX_, int PY_>
 struct Wg6WGeom {
   static constexpr int NS = 2;
@@ -359,7 +368,14 @@ __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, c
   constexpr int XQ = G::CIN / 4;                          // float4 per X pixel
   constexpr int XPT = G::RB * G::WS * XQ / 256;           // float4 of RB rows per thread
   constexpr int YQ = G::COUT / 4;
-  constexpr int YN = G::KPAD * YQ;
+#ifndef BA3C_W6W_UNPOOL
+#define BA3C_W6W_UNPOOL 1     // dY staged per pooled element (0: per un-pooled pixel, A/B)
+#endif
+  // UNP: each (pooled pixel, 4 channels) of dP is loaded and split once and written to the four
+  // pixels of its window with per-channel masks (as band6r_up_body); the padded pixels KP ..
+  // KPAD - 1 are zeroed once and never written again
+  constexpr bool UNP = BA3C_W6W_UNPOOL;
+  constexpr int YN = UNP ? (G::RB / 2) * G::PW * YQ : G::KPAD * YQ;
   constexpr int YPT = (YN + 255) / 256;
   float4 xv[XPT], yv[YPT];
   uint32_t yc[YPT];
@@ -376,6 +392,22 @@ __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, c
   };
   auto load_y = [&](int img, int bi) {
     const int y0 = bi * G::RB;
+    if constexpr (UNP) {
+#pragma unroll
+      for (int i = 0; i < YPT; ++i) {
+        const int f = tid + 256 * i;
+        const int oq = f % YQ, rest = f / YQ;
+        const int pc = rest % G::PW, py = (y0 >> 1) + rest / G::PW;
+        yv[i] = f4zero();
+        yc[i] = 0;
+        if (f < YN) {
+          const size_t off = ((size_t)(img * G::PH + py) * G::PW + pc) * G::COUT + oq * 4;
+          yv[i] = *reinterpret_cast<const float4*>(a.dp + off);
+          yc[i] = *reinterpret_cast<const uint32_t*>(a.code + off);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < YPT; ++i) {
       const int f = tid + 256 * i;
@@ -407,6 +439,32 @@ __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, c
   };
   auto store_y = [&](int bi) {
     const int y0 = bi * G::RB;
+    if constexpr (UNP) {
+#pragma unroll
+      for (int i = 0; i < YPT; ++i) {
+        const int f = tid + 256 * i;
+        if (f < YN) {
+          const int oq = f % YQ, rest = f / YQ;
+          const int pc = rest % G::PW, pr = rest / G::PW;
+          uint32_t s0[G::NS], s1[G::NS];
+          SP::split(yv[i].x, yv[i].y, ysc, s0);
+          SP::split(yv[i].z, yv[i].w, ysc, s1);
+          const uint32_t c01 = __builtin_amdgcn_perm(yc[i], yc[i], 0x0C010C00u);   // codes as halves
+          const uint32_t c23 = __builtin_amdgcn_perm(yc[i], yc[i], 0x0C030C02u);
+          char* base = ys + ((2 * pr) * G::WO + 2 * pc) * G::PY + oq * 8;
+#pragma unroll
+          for (int sub = 0; sub < 4; ++sub) {
+            const uint32_t S = (uint32_t)sub * 0x00010001u;
+            const uint32_t m01 = w6_mask16_eq0(c01 ^ S), m23 = w6_mask16_eq0(c23 ^ S);
+            char* d = base + ((sub >> 1) * G::WO + (sub & 1)) * G::PY;
+#pragma unroll
+            for (int sp = 0; sp < G::NS; ++sp)
+              *reinterpret_cast<uint2*>(d + sp * G::YSB) = make_uint2(s0[sp] & m01, s1[sp] & m23);
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < YPT; ++i) {
       const int f = tid + 256 * i;
@@ -427,6 +485,11 @@ __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, c
     }
   };
 
+  if constexpr (UNP) {
+    // padded pixels KP .. KPAD - 1 of dY stay zero (the pooled items never write them)
+    for (int i = tid; i < (G::KPAD - G::KP) * G::PY / 16; i += 256)
+      reinterpret_cast<uint4*>(ys + G::KP * G::PY)[i] = make_uint4(0, 0, 0, 0);
+  }
   int band = img0 * G::NBANDS;
   if (band < band_end) {
     load_x(img0, G::HALO, xv);
