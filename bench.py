@@ -392,6 +392,7 @@ def main():
            "step_frac_of_bf16x6_peak": round(step_tflops / kernel_peak(6), 4),
            "step_vs_fp32_mfma_peak": round(step_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
            "roofline": roof,
+           "probe": {"kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": launches},
            "kernel_ms_one_step": {k: round(v, 4) for k, v in per_kernel.items()}}
 
     if world > 1:

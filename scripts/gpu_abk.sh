@@ -20,5 +20,5 @@ for f in gpurun_out/$tag/bench_*.log; do
   grep -h '^{' $f | python -c "
 import sys,json
 for l in sys.stdin:
-    d=json.loads(l); r=d['roofline']; print('%-40s' % '$f'.split('/')[-1], d['value'], d['ms_per_step'], r['kernel'], r['avg_launch_ms'], r['frac'])"
+    d=json.loads(l); r=d['probe']; print('%-40s' % '$f'.split('/')[-1], d['value'], d['ms_per_step'], r['kernel'], r['avg_launch_ms'], (d['roofline'] or {}).get('frac'))"
 done
