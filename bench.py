@@ -60,6 +60,20 @@ KERNEL_LAYER = {"conv0_fwd": "conv0", "conv1_fwd": "conv1", "conv2_fwd": "conv2"
                 "conv3_wgrad": "conv3", "fc1_wgrad": "fc1"}
 
 
+def probe_flops(dom, per_kernel, macs, B):
+    """Algorithmic FLOPs of one launch of the probed kernel id.  An input-gradient launch that
+    also ran its layer's weight gradient (multi-job launch: that weight-gradient id then records
+    no launch of its own, 0.0 in the one-step probe) counts both products."""
+    layer = KERNEL_LAYER.get(dom)
+    if layer is None:
+        return None, [dom]
+    jobs, flops = [dom], 2.0 * macs[layer] * B
+    if dom.endswith("_dgrad") and per_kernel.get(layer + "_wgrad", 1.0) == 0.0:
+        jobs.append(layer + "_wgrad")
+        flops *= 2
+    return flops, jobs
+
+
 def train_step_flops(B, C, F, A=4):
     """fwd + wgrad(all) + dgrad(all but conv0), real input channels."""
     m = layer_macs(C, F)
@@ -353,7 +367,7 @@ def main():
     ms_step = elapsed / args.steps * 1000.0
     C = 4
     macs = layer_macs(C, F)
-    dom_flops = 2.0 * macs[KERNEL_LAYER[dom]] * B if dom in KERNEL_LAYER else None
+    dom_flops, dom_jobs = probe_flops(dom, per_kernel, macs, B)
     avg_ms = probe_ms / max(launches, 1)
     roof = None
     if dom_flops:
@@ -367,7 +381,7 @@ def main():
             path = "fp16 MFMA, %d products per fp32 product (power-of-two scaled hi/lo split)" % split
         else:
             path = "bf16 MFMA, %d products per fp32 product (exact hi/mid/lo split)" % split
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2),
+        roof = {"bound": "mfma", "kernel": dom, "jobs": dom_jobs, "achieved": round(ach, 2),
                 "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "traffic": pmc_traffic(dom), "avg_launch_ms": round(avg_ms, 4),
                 "launches": launches, "path": path,

@@ -75,6 +75,8 @@ struct ba3c_handle {
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  bool c1pair = true;   // conv1 input + weight gradients as one multi-job launch at large batch
+                        // (BA3C_C1PAIR=0: two launches)
   bool w6w = true;    // conv1 weight gradient, B >= W6W_MIN_B: all channels per workgroup
                       // (BA3C_W6W=0: two 16-channel groups, wgrad6_kernel)
   // conv1 fwd / dgrad on the pipelined persistent band kernel (BA3C_PIPE=1).  Off: r02e
@@ -206,6 +208,11 @@ inline int conv1_wgrad_p(int B) { return std::max(64, std::min(W6_P1, B * 9 / 4)
 // batch on: whole images per workgroup, two workgroups per CU, one slab each
 constexpr int W6W_MIN_B = 512, W6W_P = 512;
 static_assert(W6W_P <= WG_P1, "conv1 partial slabs: the allocation covers WG_P1 slabs");
+// its slab count: one per CU (whole images, B / CUs each) where the input gradient can run beside
+// it in one launch (conv1_pair), else up to W6W_P; a function of B and the CU count alone, so
+// the paired and the separate launches sum the same slabs bit for bit
+inline bool conv1_pair_geometry(int B, int cus) { return B >= 2 * W6W_MIN_B && B % cus == 0 && cus <= WG_P1; }
+inline int conv1_w6w_p(int B, int cus) { return conv1_pair_geometry(B, cus) ? cus : std::min(W6W_P, B); }
 constexpr int FW_P0S = 512;   // conv0s_fwd_kernel: persistent, two workgroups per CU
 constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
@@ -962,12 +969,24 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
         s, da, dim3(B * LY::C1D::G::NBANDS), wa, wg)));
     CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[1]].offset));
   } else {
-    bool done = false;
+    bool done = false, paired = false;
     if constexpr (NS == 2) {
-      if (h->band && h->w6 && h->w6w && B >= W6W_MIN_B) {
+      // conv1 input and weight gradients in one launch, one workgroup of each per CU (each job
+      // walks twice the images of its separate launch)
+      if (h->band && h->b6 && h->w6 && h->w6w && h->c1pair && h->ring && conv1_pair_geometry(B, h->cus)) {
         using GW = typename LY::W1W;
         const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
-        const int P = std::min(W6W_P, B);
+        const Band6Args da = band6_args<typename LY::C1D>(h, BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B},
+                                                         w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0});
+        CHECK((launch_multi<true, Band6RJob<typename LY::C1D>, Wg6WJob<GW>>(
+            s, da, dim3(h->cus), wa, dim3(h->cus), 0, dim3(0, 1, 1), h, BA3C_K_CONV1_DGRAD)));
+        CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, h->cus, grads + h->tensors[h->idx_conv[1]].offset));
+        done = paired = true;
+      }
+      if (!done && h->band && h->w6 && h->w6w && B >= W6W_MIN_B) {
+        using GW = typename LY::W1W;
+        const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
+        const int P = conv1_w6w_p(B, h->cus);
         {
           ProbeScope ps(h, ws, BA3C_K_CONV1_WGRAD);
           hipLaunchKernelGGL(wgrad6w_kernel<GW>, dim3(P), dim3(256), 0, ws, wa);
@@ -991,7 +1010,9 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_CONV1_WGRAD, g, pl.S)));
       CHECK(conv_reduce(pl, 1, 32, 32, w.part_1));
     }
-    if (h->band) {
+    if (paired) {
+      // both gradients ran in the multi-job launch above
+    } else if (h->band) {
       const BandArgs ba{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B};
       CHECK(launch_bandx<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0},
                                           true));
@@ -1115,6 +1136,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_W6W")) h->w6w = !(e[0] == '0');
+  if (const char* e = getenv("BA3C_C1PAIR")) h->c1pair = !(e[0] == '0');
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
   if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
   if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 3;

@@ -32,6 +32,27 @@ struct Band6Job {
   }
 };
 
+// ring-walk band kernel as a job: x = first image group, gx = the job's own grid size
+template <class L>
+struct Band6RJob {
+  using Args = Band6Args;
+  static constexpr int LDS = L::LDS_BYTES;
+  __device__ static void run(const Args& a, int x, int, int, int gx, char* lds, uint32_t*) {
+    if constexpr (L::G::SRC == 1 && L::NS == 2) band6r_up_body<L>(a, x, gx, lds);
+    else band6r_body<L>(a, x, gx, lds);
+  }
+};
+
+// whole-channel weight gradient as a job
+template <class G>
+struct Wg6WJob {
+  using Args = Wg6Args;
+  static constexpr int LDS = G::X_BYTES + G::Y_BYTES;
+  __device__ static void run(const Args& a, int x, int, int, int gx, char* lds, uint32_t* red4) {
+    wgrad6w_body<G>(a, x, gx, lds, red4);
+  }
+};
+
 template <class G>
 struct Wg6Job {
   using Args = Wg6Args;
