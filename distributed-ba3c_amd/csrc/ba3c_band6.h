@@ -98,6 +98,15 @@ struct Band6Args {
   uint32_t* amax_out;
 };
 
+// packed 16-bit halves: 0xFFFF where the half is zero, else 0 (code-mask of the pooled staging)
+__device__ __forceinline__ uint32_t mask16_eq0(uint32_t d) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  u16x2 x = __builtin_bit_cast(u16x2, d);
+  x = __builtin_elementwise_min(x, (u16x2){1, 1});   // 0 where the half matched, else 1
+  x = x + (u16x2){0xFFFF, 0xFFFF};                    // 0xFFFF where matched, else 0
+  return __builtin_bit_cast(uint32_t, x);
+}
+
 // Staging and compute of one band, shared by the one-band-per-workgroup kernel and the
 // pipelined persistent kernel below.
 template <class L>
@@ -161,6 +170,71 @@ struct Band6Ops {
 #pragma unroll
     for (int sp = 0; sp < L::NS; ++sp) *reinterpret_cast<uint2*>(p + sp * L::SPB) = make_uint2(s0[sp], s1[sp]);
   }
+#ifndef BA3C_UNPOOL_STAGE
+#define BA3C_UNPOOL_STAGE 1   // 0: A/B build with the per-pixel staging (store1) everywhere
+#endif
+  // Whole-map input-gradient bands (conv2's): the zero-padded un-pooled dY staged from the
+  // POOLED map, each (pooled pixel, 4 channels) loaded and split once and written to its 2x2
+  // window with per-channel masks (mask16_eq0 on the codes as 16-bit halves); store1 instead
+  // loads and splits every staged float4 (4 loads + 4 splits per pooled element, 3 of zeros).
+  // The padding cells are zeroed in phase 0 and never written again.  Same LDS image bit for bit.
+  static constexpr bool UPSTAGE = BA3C_UNPOOL_STAGE && G::SRC == 1 && L::NS == 2 && G::NBANDS == 1 &&
+                                  G::UHO == 2 * G::UPH && G::UWO == 2 * G::UPW &&
+                                  G::UHO + 2 * G::PADY == G::HS && G::UWO + 2 * G::PADX == G::WS &&
+                                  G::PADY % 2 == 0 && G::PADX % 2 == 0;
+  __device__ static void stage_up(const Band6Args& a, char* lds, int t, int img, int ph, float asc) {
+    using SP = SplitP<L::NS>;
+    constexpr int PARTS = L::NS * L::SPB / 16;             // uint4 per staged pixel
+    if (ph == 0) {
+      constexpr int NZ = G::SROWS * G::WS * PARTS;
+      for (int f = t; f < NZ; f += 256) {
+        const int cell = f / PARTS, part = f - cell * PARTS;
+        const int r = cell / G::WS, x = cell - r * G::WS;
+        if ((unsigned)(r - G::PADY) >= (unsigned)G::UHO || (unsigned)(x - G::PADX) >= (unsigned)G::UWO)
+          *reinterpret_cast<uint4*>(lds + r * L::RP + x * L::PP + part * 16) = make_uint4(0, 0, 0, 0);
+      }
+    }
+    constexpr int NPI = G::UPH * G::UPW * (int)Q;
+    constexpr int IT = (NPI + 255) / 256;
+    float4 v[IT];
+    uint32_t c[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int f = t + 256 * i;
+      v[i] = f4zero();
+      c[i] = 0;
+      if (f < NPI) {
+        const int cq = f % Q, rest = f / Q;
+        const size_t off = ((size_t)img * (G::UPH * G::UPW) + rest) * G::CIN + ph * L::KPH + cq * 4;
+        v[i] = *reinterpret_cast<const float4*>(a.src + off);
+        c[i] = *reinterpret_cast<const uint32_t*>(a.code + off);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int f = t + 256 * i;
+      if (f < NPI) {
+        const int cq = f % Q, rest = f / Q;
+        const int pc = rest % G::UPW, py = rest / G::UPW;
+        uint32_t s0[2], s1[2];
+        SP::split(v[i].x, v[i].y, asc, s0);
+        SP::split(v[i].z, v[i].w, asc, s1);
+        const uint32_t c01 = __builtin_amdgcn_perm(c[i], c[i], 0x0C010C00u);   // codes as halves
+        const uint32_t c23 = __builtin_amdgcn_perm(c[i], c[i], 0x0C030C02u);
+        char* base = lds + (G::PADY + 2 * py) * L::RP + (G::PADX + 2 * pc) * L::PP + cq * 8;
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub) {
+          const uint32_t S = (uint32_t)sub * 0x00010001u;
+          const uint32_t m01 = mask16_eq0(c01 ^ S), m23 = mask16_eq0(c23 ^ S);
+          char* p = base + (sub >> 1) * L::RP + (sub & 1) * L::PP;
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp)
+            *reinterpret_cast<uint2*>(p + sp * L::SPB) = make_uint2(s0[sp] & m01, s1[sp] & m23);
+        }
+      }
+    }
+  }
+
   // loads in chunks of NPT (<= NPTMAX), then their stores
   template <int NPTMAX = 8>
   __device__ static void stage(const Band6Args& a, char* lds, int t, int img, int y0, int rows_out, int ph,
@@ -385,12 +459,14 @@ __device__ __forceinline__ void band6_body(const Band6Args& a, int bx, char* lds
   float omax = 0.f;
   // every staging load of the band in flight at once (one global round trip, not two)
   if constexpr (L::NPH == 1) {
-    O::template stage<BA3C_STAGE_NPT>(a, lds, tid, img, y0, rows_out, 0, asc);
+    if constexpr (O::UPSTAGE) O::stage_up(a, lds, tid, img, 0, asc);
+    else O::template stage<BA3C_STAGE_NPT>(a, lds, tid, img, y0, rows_out, 0, asc);
     __syncthreads();
   }
   O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [&](int ph) {
     if (ph) __syncthreads();                                // previous phase's reads are done
-    O::template stage<BA3C_STAGE_NPT>(a, lds, tid, img, y0, rows_out, ph, asc);
+    if constexpr (O::UPSTAGE) O::stage_up(a, lds, tid, img, ph, asc);
+    else O::template stage<BA3C_STAGE_NPT>(a, lds, tid, img, y0, rows_out, ph, asc);
     __syncthreads();
   });
   if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
@@ -501,13 +577,6 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
 // 16-bit halves); the padding columns are zeroed once per workgroup and never written again,
 // padding rows are written as zeros.  Split values of zero are +0 either way, so the staged LDS
 // image is bit for bit the one store1 builds.
-__device__ __forceinline__ uint32_t mask16_eq0(uint32_t d) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  u16x2 x = __builtin_bit_cast(u16x2, d);
-  x = __builtin_elementwise_min(x, (u16x2){1, 1});   // 0 where the half matched, else 1
-  x = x + (u16x2){0xFFFF, 0xFFFF};                    // 0xFFFF where matched, else 0
-  return __builtin_bit_cast(uint32_t, x);
-}
 
 template <class L>
 __device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int gx, char* lds) {
@@ -611,9 +680,6 @@ __device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int g
   }
 }
 
-#ifndef BA3C_UNPOOL_STAGE
-#define BA3C_UNPOOL_STAGE 1   // 0: A/B build with the per-pixel staging (Band6Ops::store1)
-#endif
 template <class L, bool PRE_ = L::G::SRC == 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6r_kernel(const Band6Args a) {
   __shared__ uint4 lds4[L::LDS_BYTES / 16];

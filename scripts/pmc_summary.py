@@ -18,9 +18,9 @@ SHORT = [  # (regex on the kernel symbol, bench kernel id)
     (r"conv0s_wgrad_kernel", "conv0_wgrad"),
     (r"conv_band6[rp]?_kernel<.*BandGeom<40, 40, 32, 32", "conv1_fwd"),
     (r"conv_band6[rp]?_kernel<.*BandGeom<18, 18, 32, 64", "conv2_fwd"),
-    (r"conv_band6[rp]?_kernel<.*BandGeom<44, 44, 32, 32", "conv1_dgrad"),
+    (r"(conv_band6[rp]?_kernel|multi_kernel_w2)<.*BandGeom<44, 44, 32, 32", "conv1_dgrad"),
     (r"(conv_band6[rp]?_kernel|multi_kernel_w2)<.*BandGeom<22, 22, 64, 32", "conv2_dgrad"),
-    (r"wgrad6?_(band_)?kernel<.*Geom<40, 40, 32", "conv1_wgrad"),
+    (r"wgrad6?w?_(band_)?kernel<.*Geom<40, 40, 32", "conv1_wgrad"),
     (r"wgrad6?_(band_)?kernel<.*Geom<18, 18, 32", "conv2_wgrad"),
     (r"ConvFwd<false, 7, 7, 64", "conv3_fwd"),
     (r"ConvDgrad<7, 7, 64", "conv3_dgrad"),
