@@ -60,18 +60,14 @@ KERNEL_LAYER = {"conv0_fwd": "conv0", "conv1_fwd": "conv1", "conv2_fwd": "conv2"
                 "conv3_wgrad": "conv3", "fc1_wgrad": "fc1"}
 
 
-def probe_flops(dom, per_kernel, macs, B):
-    """Algorithmic FLOPs of one launch of the probed kernel id.  An input-gradient launch that
-    also ran its layer's weight gradient (multi-job launch: that weight-gradient id then records
-    no launch of its own, 0.0 in the one-step probe) counts both products."""
-    layer = KERNEL_LAYER.get(dom)
-    if layer is None:
-        return None, [dom]
-    jobs, flops = [dom], 2.0 * macs[layer] * B
-    if dom.endswith("_dgrad") and per_kernel.get(layer + "_wgrad", 1.0) == 0.0:
-        jobs.append(layer + "_wgrad")
-        flops *= 2
-    return flops, jobs
+def probe_flops(dom, merged, macs, B):
+    """Algorithmic FLOPs of one launch of the probed kernel id, including the kernels that ran
+    inside the same multi-job launch (`merged`, from ba3c_kernel_merged: they record no launch
+    of their own)."""
+    jobs = [dom] + [k for k in merged if k in KERNEL_LAYER]
+    if any(k not in KERNEL_LAYER for k in jobs):
+        return None, jobs
+    return sum(2.0 * macs[KERNEL_LAYER[k]] * B for k in jobs), jobs
 
 
 def train_step_flops(B, C, F, A=4):
@@ -367,15 +363,22 @@ def main():
     ms_step = elapsed / args.steps * 1000.0
     C = 4
     macs = layer_macs(C, F)
-    dom_flops, dom_jobs = probe_flops(dom, per_kernel, macs, B)
+    dom_flops, dom_jobs = probe_flops(dom, tr.engine.kernel_merged(dom), macs, B)
+    # a multi-job launch's ceiling: its total FLOPs over the time every job would take at the
+    # peak of its own arithmetic path
+    job_peak_s = sum(2.0 * macs[KERNEL_LAYER[k]] * B / (kernel_peak(tr.engine.kernel_split(k)) * 1e12)
+                     for k in dom_jobs) if dom_flops else None
     avg_ms = probe_ms / max(launches, 1)
     roof = None
     if dom_flops:
         split = tr.engine.kernel_split(dom)
         fam = tr.engine.kernel_family(dom)
-        peak = kernel_peak(split)
+        peak = dom_flops / job_peak_s / 1e12
         ach = dom_flops / (avg_ms / 1000.0) / 1e12
-        if split <= 1:
+        if len(dom_jobs) > 1:
+            path = "multi-job launch %s: %s" % ("+".join(dom_jobs), ", ".join(
+                "%s %d products per fp32 product" % (k, tr.engine.kernel_split(k)) for k in dom_jobs))
+        elif split <= 1:
             path = "fp32 MFMA"
         elif fam == 2:
             path = "fp16 MFMA, %d products per fp32 product (power-of-two scaled hi/lo split)" % split
@@ -387,7 +390,8 @@ def main():
                 "launches": launches, "path": path,
                 "peak_basis": "algorithmic fp32 FLOP/s: %s" % (
                     "fp32 MFMA 157.3 TF" if split <= 1 else
-                    "2516.6 TF dense 16-bit MFMA / %d split products" % split)}
+                    "2516.6 TF dense 16-bit MFMA / %d split products" % split if len(dom_jobs) == 1 else
+                    "total FLOPs / sum over jobs of (job FLOPs / 2516.6 TF x its split products)")}
     step_tflops = train_step_flops(B, C, F, A) / (ms_step / 1000.0) / 1e12
 
     out = {"metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,

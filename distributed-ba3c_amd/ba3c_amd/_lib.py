@@ -38,6 +38,8 @@ class Ba3cOptParams(ctypes.Structure):
 
 
 _lib = None
+# roofline-accounting queries an alternative A/B build (BA3C_LIB) may predate
+AB_OPTIONAL = {"ba3c_kernel_merged"}
 
 
 def load():
@@ -82,12 +84,15 @@ def load():
         "ba3c_probe_read": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]),
         "ba3c_device_errors": (i32, [P, ctypes.POINTER(ctypes.c_uint32)]),
         "ba3c_kernel_split": (i32, [P, i32]),
+        "ba3c_kernel_merged": (i32, [P, i32]),
         "ba3c_kernel_family": (i32, [P, i32]),
         "ba3c_nstep_returns": (i32, [P, P, P, P, P, P, i32, i32, ctypes.c_double, P, P, P, P, P]),
         "ba3c_gather_rows": (i32, [P, P, P, i32, i64, P]),
         "ba3c_history_push": (i32, [P, P, P, P, i32, i32, i32, i32]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("BA3C_LIB") and name in AB_OPTIONAL and not hasattr(lib, name):
+            continue            # an A/B build older than this accounting query
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

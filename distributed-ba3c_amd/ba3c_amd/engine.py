@@ -225,6 +225,14 @@ class Ba3cEngine(object):
         kid = -1 if kernel is None else _lib.KERNEL_IDS[kernel]
         _lib.check(self.lib.ba3c_probe_enable(self.h, kid))
 
+    def kernel_merged(self, kernel):
+        """Kernel names that ran inside `kernel`'s launch in the last training pass (multi-job
+        launches; ba3c_kernel_merged)."""
+        if not hasattr(self.lib, "ba3c_kernel_merged"):
+            return []
+        m = int(self.lib.ba3c_kernel_merged(self.h, _lib.KERNEL_IDS[kernel]))
+        return [] if m <= 0 else [k for k, i in _lib.KERNEL_IDS.items() if m >> i & 1]
+
     def kernel_split(self, kernel):
         """16-bit MFMA products per fp32 product of `kernel` on this handle (6: bf16 hi/mid/lo,
         3: scaled fp16 hi/lo or conv0's u8 x bf16x3, 2: conv0's u8 x fp16 hi/lo, 1: fp32 MFMA,

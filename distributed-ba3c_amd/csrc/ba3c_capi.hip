@@ -75,8 +75,10 @@ struct ba3c_handle {
   bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
   bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
   bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
-  bool c1pair = true;   // conv1 input + weight gradients as one multi-job launch at large batch
-                        // (BA3C_C1PAIR=0: two launches)
+  // large batches: conv1's weight gradient shares a launch with (2, default) conv0's weight
+  // gradient, (1) conv1's input gradient, or (0) runs alone (BA3C_C1PAIR)
+  int c1pair = 2;
+  uint32_t merged[BA3C_NUM_KERNELS] = {};   // ba3c_kernel_merged, per training pass
   bool w6w = true;    // conv1 weight gradient, B >= W6W_MIN_B: all channels per workgroup
                       // (BA3C_W6W=0: two 16-channel groups, wgrad6_kernel)
   // conv1 fwd / dgrad on the pipelined persistent band kernel (BA3C_PIPE=1).  Off: r02e
@@ -782,6 +784,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   const float* W2c = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3c = prm + h->tensors[h->idx_conv[3]].offset;
   const float* Wfc = prm + h->tensors[h->idx_fc1].offset;
+  if (phase != 2) std::memset(h->merged, 0, sizeof(h->merged));   // a new training pass
+  bool defer_w1 = false;   // conv1's weight gradient waits for conv0's (one paired launch)
   // The weight-gradient kernels (heads, fc1, conv3..conv1) run on the side stream `ws`,
   // each after the event that publishes its output gradient; the input-gradient chain and
   // conv0's weight gradient (own partials region) stay on `s`, which joins `ws` at the end.
@@ -842,7 +846,9 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
     const dim3 gd((d.M + 63) / 64, (d.N + 63) / 64, 1), gh((pl.M + 127) / 128, (pl.N + 31) / 32, pl.S),
         gff((plf.M + 127) / 128, (plf.N + 63) / 64, plf.S);
-    if (mj_fc && !big)   // fc1 input gradient + head and fc1 weight gradients: one launch
+    if (mj_fc)   // fc1 input gradient + head and fc1 weight gradients: one launch
+      h->merged[BA3C_K_FC1_DGRAD] |= (1u << BA3C_K_FC1_WGRAD) | (1u << BA3C_K_HEAD_WGRAD);
+    if (mj_fc && !big)
       CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, 4>, Gemm6Job<128, 32, 4, 1, BatchWgrad, 4>,
                           Gemm6Job<128, 64, 2, 2, BatchWgrad, 4>>(s, d, gd, g, gh, gf, gff, h, BA3C_K_FC1_DGRAD)));
     else if (mj_fc)
@@ -907,6 +913,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     if (mj) {
       CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, decltype(d), 4, 2>, Gemm6Job<128, 64, 4, 1, decltype(g), 4, 2>,
                           NoJob, true>(s, d, gd, g, gw, 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
+      h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_CONV3_WGRAD;
     } else {
       if (big) CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
       else CHECK((launch_gemm<128, 64, 4, 1, decltype(g), 2>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
@@ -923,6 +930,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
                                                       w, WT_C2D, SplitIO{AM_DP2, 3, AM_DP1});
     CHECK((launch_multi<true, Band6Job<typename LY::C2DS>, Wg6Job<typename LY::W2>>(
         s, da, dim3(B * LY::C2DS::G::NBANDS), wa, wg)));
+    h->merged[BA3C_K_CONV2_DGRAD] |= 1u << BA3C_K_CONV2_WGRAD;
     CHECK(reduce_wgrad6<typename LY::W2>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[2]].offset));
   } else if (mj_c2) {
     const Wg6Args wa{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)};
@@ -931,6 +939,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
                                                      w, WT_C2D, SplitIO{AM_DP2, 3, AM_DP1});
     CHECK((launch_multi<true, Band6Job<typename LY::C2D>, Wg6Job<typename LY::W2>>(
         s, da, dim3(B * LY::C2D::G::NBANDS), wa, wg, 0, dim3(0, 1, 1), h, BA3C_K_CONV2_DGRAD)));
+    h->merged[BA3C_K_CONV2_DGRAD] |= 1u << BA3C_K_CONV2_WGRAD;
     CHECK(reduce_wgrad6<typename LY::W2>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[2]].offset));
   } else {
     if (h->band && h->w6) {
@@ -967,19 +976,25 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
                                                      w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0});
     CHECK((launch_multi<true, Band6Job<typename LY::C1D>, Wg6Job<typename LY::W1>>(
         s, da, dim3(B * LY::C1D::G::NBANDS), wa, wg)));
+    h->merged[BA3C_K_CONV1_DGRAD] |= 1u << BA3C_K_CONV1_WGRAD;
     CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[1]].offset));
   } else {
     bool done = false, paired = false;
     if constexpr (NS == 2) {
+      const bool pairgeo = h->band && h->b6 && h->w6 && h->w6w && h->ring && conv1_pair_geometry(B, h->cus);
+      if (pairgeo && h->c1pair == 2 && CH == 4 && h->split) {
+        done = defer_w1 = true;                             // beside conv0's weight gradient below
+      }
       // conv1 input and weight gradients in one launch, one workgroup of each per CU (each job
       // walks twice the images of its separate launch)
-      if (h->band && h->b6 && h->w6 && h->w6w && h->c1pair && h->ring && conv1_pair_geometry(B, h->cus)) {
+      if (!done && pairgeo && h->c1pair == 1) {
         using GW = typename LY::W1W;
         const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
         const Band6Args da = band6_args<typename LY::C1D>(h, BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B},
                                                          w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0});
         CHECK((launch_multi<true, Band6RJob<typename LY::C1D>, Wg6WJob<GW>>(
             s, da, dim3(h->cus), wa, dim3(h->cus), 0, dim3(0, 1, 1), h, BA3C_K_CONV1_DGRAD)));
+        h->merged[BA3C_K_CONV1_DGRAD] |= 1u << BA3C_K_CONV1_WGRAD;
         CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, h->cus, grads + h->tensors[h->idx_conv[1]].offset));
         done = paired = true;
       }
@@ -1023,10 +1038,24 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   }
   // conv0 (no input gradient: the frames are not trainable)
   if (h->band && CH == 4 && h->split) {
-    const int P = std::min(WG_P0S, B * Conv0W<NS>::NBANDS);
-    {
+    // slab count: one per CU where conv1's weight gradient can share the launch (on every launch
+    // path, so they all sum the same slabs), else up to WG_P0S
+    const int P = (NS == 2 && conv1_pair_geometry(B, h->cus)) ? h->cus
+                                                              : std::min(WG_P0S, B * Conv0W<NS>::NBANDS);
+    const Conv0WArgs a0{state, w.dp0, w.c0, w.part0, B, w.am(AM_DP0, h)};
+    if (defer_w1) {
+      // conv1's whole-channel weight gradient (MFMA-bound) beside conv0's (VALU-bound): one
+      // workgroup of each per CU, one launch (ba3c_conv0.hip)
+      const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
+      {
+        ProbeScope ps(h, s, BA3C_K_CONV0_WGRAD);
+        HIP_TRY(launch_wgrad01_pair(s, wa, h->cus, a0, P));
+      }
+      h->merged[BA3C_K_CONV0_WGRAD] |= 1u << BA3C_K_CONV1_WGRAD;
+      CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, h->cus, grads + h->tensors[h->idx_conv[1]].offset));
+    } else {
       ProbeScope ps(h, s, BA3C_K_CONV0_WGRAD);
-      HIP_TRY(launch_conv0s_wgrad(NS, dim3(P), s, Conv0WArgs{state, w.dp0, w.c0, w.part0, B, w.am(AM_DP0, h)}));
+      HIP_TRY(launch_conv0s_wgrad(NS, dim3(P), s, a0));
     }
     HIP_TRY(hipGetLastError());
     ReduceMap mp{};
@@ -1136,7 +1165,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_W6W")) h->w6w = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_C1PAIR")) h->c1pair = !(e[0] == '0');
+  if (const char* e = getenv("BA3C_C1PAIR")) h->c1pair = e[0] - '0';
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
   if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
   if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 3;
@@ -1598,6 +1627,11 @@ int ba3c_kernel_split(const ba3c_handle* h, int32_t kid) {
     case BA3C_K_UPDATE: return 0;
     default: return 1;
   }
+}
+
+int ba3c_kernel_merged(const ba3c_handle* h, int32_t kid) {
+  if (!h || kid < 0 || kid >= BA3C_NUM_KERNELS) return -1;
+  return (int)h->merged[kid];
 }
 
 int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {

@@ -9,6 +9,7 @@
 
 #include "ba3c_launch.h"
 #include "ba3c_split.h"
+#include "ba3c_wgrad6.h"
 
 namespace ba3c {
 
@@ -17,6 +18,26 @@ hipError_t launch_conv0s_fwd(int ns, int lay, dim3 grid, hipStream_t s, const Co
   else if (ns == 2) hipLaunchKernelGGL((conv0s_fwd_kernel<2, 2>), grid, dim3(256), 0, s, a);
   else if (lay == 3) hipLaunchKernelGGL((conv0s_fwd_kernel<3, 3>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((conv0s_fwd_kernel<3, 2>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// conv1's whole-channel weight gradient (wgrad6w_body, MFMA-bound) beside conv0's weight
+// gradient (VALU-bound un-pooling) in one launch: blocks [0, g1) walk conv1's images, blocks
+// [g1, g1 + g0) conv0's bands, one workgroup of each per CU.  Both read only the finished
+// output gradients dP1 / dP0 and write their own partial slabs; each body runs exactly as in
+// its plain kernel with (bx, gx) = (block - first block of its job, job grid).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+wgrad01_pair_kernel(const Wg6Args a1, const Conv0WArgs a0, int g1, int g0) {
+  constexpr int B1 = Conv1W6W::X_BYTES + Conv1W6W::Y_BYTES, B0 = Conv0W<2>::ALLOC_U4 * 16;
+  __shared__ uint4 lds[(B1 > B0 ? B1 : B0) / 16];
+  __shared__ uint32_t red4[4];
+  const int b = blockIdx.x;
+  if (b < g1) wgrad6w_body<Conv1W6W>(a1, b, g1, reinterpret_cast<char*>(lds), red4);
+  else conv0s_wgrad_body<2>(a0, b - g1, g0, lds, red4);
+}
+
+hipError_t launch_wgrad01_pair(hipStream_t s, const Wg6Args& a1, int g1, const Conv0WArgs& a0, int g0) {
+  hipLaunchKernelGGL(wgrad01_pair_kernel, dim3(g1 + g0), dim3(256), 0, s, a1, a0, g1, g0);
   return hipGetLastError();
 }
 

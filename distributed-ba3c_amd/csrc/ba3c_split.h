@@ -615,18 +615,18 @@ struct Conv0WArgs {
   const uint32_t* amax_dp; // NS = 2: per-image max |dP0| slots
 };
 
+// bx / gx: first band and persistent stride (blockIdx.x / gridDim.x of the plain kernel; a
+// paired launch passes its own); lds: Conv0W<NS>::ALLOC_U4 uint4 of LDS, red4: 4 words
 template <int NS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv0s_wgrad_kernel(const Conv0WArgs a) {
+__device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, int gx, uint4* lds, uint32_t* red4) {
   using G = Conv0W<NS>;
   using SP = SplitP<NS>;
-  __shared__ uint4 lds[G::ALLOC_U4];
   uint16_t* ys = reinterpret_cast<uint16_t*>(lds);
   uint16_t* xs = ys + G::Y_16;
   uint8_t* yc8 = reinterpret_cast<uint8_t*>(xs + G::X_16);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int nbands = a.batch * G::NBANDS;
-  __shared__ uint32_t red4[4];
   const int ky = NS == 2 ? amax_exp(amax_all(a.amax_dp, a.batch, red4)) : 0;
   const float ysc = exp2i(ky);
 
@@ -699,13 +699,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
 #pragma unroll
   for (int mt = 0; mt < G::MT; ++mt) acc[mt][0] = acc[mt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int band = blockIdx.x;
+  int band = bx;
   if (band < nbands) load_band(band);
-  for (; band < nbands; band += gridDim.x) {
+  for (; band < nbands; band += gx) {
     __syncthreads();                                   // previous band's LDS reads are done
     store_band();
     __syncthreads();
-    if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);
+    if (band + gx < nbands) load_band(band + gx);
 #pragma unroll
     for (int i = 0; i < G::KSW; ++i) {
       const int s = wave + 4 * i;
@@ -766,12 +766,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
         if (tap >= 0) red[(wave * G::M + tap * G::C + r) * G::COUT + 16 * nt + li] = acc[mt][nt][r];
       }
   __syncthreads();
-  float* pz = a.part + (size_t)blockIdx.x * G::M * G::COUT;
+  float* pz = a.part + (size_t)bx * G::M * G::COUT;
   const float oscale = (1.0f / 255.0f) * exp2i(-ky);
   for (int e = tid; e < G::M * G::COUT; e += 256) {
     constexpr int W = G::M * G::COUT;
     pz[e] = (((red[e] + red[W + e]) + red[2 * W + e]) + red[3 * W + e]) * oscale;
   }
+}
+
+template <int NS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv0s_wgrad_kernel(const Conv0WArgs a) {
+  __shared__ uint4 lds[Conv0W<NS>::ALLOC_U4];
+  __shared__ uint32_t red4[4];
+  conv0s_wgrad_body<NS>(a, blockIdx.x, gridDim.x, lds, red4);
 }
 
 }  // namespace ba3c

@@ -344,6 +344,9 @@ struct Wg6WGeom {
   static_assert(X_BYTES % 16 == 0 && (HALO * WS * PX) % 16 == 0, "wgrad6w geometry");
 };
 
+// conv1's whole-channel weight-gradient geometry (ba3c_capi.hip Lay<2>::W1W, ba3c_conv0.hip)
+using Conv1W6W = Wg6WGeom<40, 40, 32, 32, 4, 160, 160>;
+
 template <class G>
 __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
   using SP = SplitP<G::NS>;

@@ -216,6 +216,12 @@ int ba3c_kernel_split(const ba3c_handle* h, int32_t kernel_id);
  * scaled fp16 planes (v_mfma_*_f16); otherwise the value of ba3c_kernel_split (1, 0, -1). */
 int ba3c_kernel_family(const ba3c_handle* h, int32_t kernel_id);
 
+/* Kernels that ran inside kernel `kernel_id`'s launch in the last training pass (multi-job
+ * launches: the probe of `kernel_id` brackets them too, and they record no launch of their own),
+ * as a bitmask of kernel ids; 0 when the launch ran only that kernel, -1 on a bad id.  For
+ * roofline accounting only (no reference counterpart). */
+int ba3c_kernel_merged(const ba3c_handle* h, int32_t kernel_id);
+
 /* ---- data formats either side of the path ---------------- */
 
 /* n-step returns of MySimulatorMaster (OpenAIGym/train.py:408-437, _parse_memory) for n_envs
