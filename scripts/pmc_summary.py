@@ -15,7 +15,7 @@ import sys
 
 SHORT = [  # (regex on the kernel symbol, bench kernel id)
     (r"conv0s_fwd_kernel|conv0_band_kernel", "conv0_fwd"),
-    (r"conv0s_wgrad_kernel", "conv0_wgrad"),
+    (r"conv0s_wgrad_kernel|wgrad01_pair_kernel", "conv0_wgrad"),
     (r"conv_band6[rp]?_kernel<.*BandGeom<40, 40, 32, 32", "conv1_fwd"),
     (r"conv_band6[rp]?_kernel<.*BandGeom<18, 18, 32, 64", "conv2_fwd"),
     (r"(conv_band6[rp]?_kernel|multi_kernel_w2)<.*BandGeom<44, 44, 32, 32", "conv1_dgrad"),
