@@ -32,8 +32,14 @@ wgrad01_pair_kernel(const Wg6Args a1, const Conv0WArgs a0, int g1, int g0) {
   __shared__ uint4 lds[(B1 > B0 ? B1 : B0) / 16];
   __shared__ uint32_t red4[4];
   const int b = blockIdx.x;
-  if (b < g1) wgrad6w_body<Conv1W6W>(a1, b, g1, reinterpret_cast<char*>(lds), red4);
-  else conv0s_wgrad_body<2>(a0, b - g1, g0, lds, red4);
+#ifndef BA3C_DIAG_PAIR
+#define BA3C_DIAG_PAIR 0      // diagnostics only (A/B timing): 1 = conv1 job skipped, 2 = conv0 job skipped
+#endif
+  if (b < g1) {
+    if (BA3C_DIAG_PAIR != 1) wgrad6w_body<Conv1W6W>(a1, b, g1, reinterpret_cast<char*>(lds), red4);
+  } else if (BA3C_DIAG_PAIR != 2) {
+    conv0s_wgrad_body<2>(a0, b - g1, g0, lds, red4);
+  }
 }
 
 hipError_t launch_wgrad01_pair(hipStream_t s, const Wg6Args& a1, int g1, const Conv0WArgs& a0, int g0) {
