@@ -205,7 +205,10 @@ constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workg
 // conv1 weight-gradient workgroups: ~4 bands each, at least 64 (at B=32 one band per
 // workgroup made 256 partial slabs of 100 KB — 26 MB written and read back by the reduction
 // for 3.3 MB of input).  A function of B alone, so every launch path sums the same slabs.
-inline int conv1_wgrad_p(int B) { return std::max(64, std::min(W6_P1, B * 9 / 4)); }
+#ifndef BA3C_C1W_BPW
+#define BA3C_C1W_BPW 3        // conv1 weight-gradient bands per workgroup below the ring sizes (r03: 4 -> 3, B=32 0.1966 -> 0.1925 ms)
+#endif
+inline int conv1_wgrad_p(int B) { return std::max(64, std::min(W6_P1, B * 9 / BA3C_C1W_BPW)); }
 // conv1 weight gradient with all 32 input channels per workgroup (wgrad6w_kernel) from this
 // batch on: whole images per workgroup, two workgroups per CU, one slab each
 constexpr int W6W_MIN_B = 512, W6W_P = 512;
