@@ -209,3 +209,21 @@ def test_launcher_flags_build_the_reference_configuration():
     check_distributed(b, 1)
     with pytest.raises(SystemExit):
         check_distributed(b, 2)              # no asynchronous multi-GPU mode
+
+
+def test_bench_prices_multi_job_launches_with_all_their_jobs():
+    """bench.py roofline accounting: a multi-job launch (ba3c_kernel_merged) counts every job's
+    algorithmic FLOPs, and its peak is the total over the time each job would take at its own
+    path's peak (conv0's u8 x fp16 hi/lo at 2 products, conv1's fp16x3 at 3)."""
+    import bench
+    B = 2048
+    macs = bench.layer_macs(4, 512)
+    f, jobs = bench.probe_flops("conv0_wgrad", ["conv1_wgrad", "wgrad_reduce"], macs, B)
+    assert jobs == ["conv0_wgrad", "conv1_wgrad"]
+    assert f == 2.0 * (macs["conv0"] + macs["conv1"]) * B
+    f1, j1 = bench.probe_flops("conv1_dgrad", [], macs, B)
+    assert j1 == ["conv1_dgrad"] and f1 == 2.0 * macs["conv1"] * B
+    assert bench.probe_flops("heads", [], macs, B)[0] is None
+    t = 2.0 * macs["conv0"] * B / (bench.kernel_peak(2) * 1e12) + \
+        2.0 * macs["conv1"] * B / (bench.kernel_peak(3) * 1e12)
+    assert abs(f / t / 1e12 - 961.2) < 0.5          # the r03b line's combined peak
