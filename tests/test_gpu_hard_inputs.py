@@ -231,3 +231,34 @@ def test_greedy_eval_action_matches_numpy_argmax():
     want = np.where(u < 0.001, rand, np.argmax(probs, axis=1))
     got = eng.greedy(dev(probs), dev(u), dev(rand), eps=0.001).cpu().numpy()
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_conv1_launch_pairings_match_default(monkeypatch, mode):
+    """conv1's large-batch backward launch structure (BA3C_C1PAIR): 2 (default) = input gradient
+    alone, then conv1's weight gradient beside conv0's in one launch; 1 = conv1 input + weight
+    gradients in one launch; 0 = separate launches.  Every variant sums the same slabs in the
+    same order (one per CU in the pair geometry), so the gradients, scalars and dP0 are
+    bit-identical — B=1024, 4 images per ring-walk workgroup."""
+    B = 1024
+    rs = np.random.RandomState(83)
+    state = dev(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8))
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    params = O.init_params(512, 1, 4, seed=12, dtype=np.float32)
+    out = []
+    for env in (None, mode):
+        if env is None:
+            monkeypatch.delenv("BA3C_C1PAIR", raising=False)
+        else:
+            monkeypatch.setenv("BA3C_C1PAIR", env)
+        eng = _engine(B)
+        eng.load_params(params)
+        sc = eng.train_grads(state, action, R)
+        dp0 = eng.workspace_tensor("dp0", B).clone()
+        torch.cuda.synchronize()
+        out.append((eng.grads.clone(), sc.clone(), dp0))
+        del eng
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
