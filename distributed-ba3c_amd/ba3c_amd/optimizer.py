@@ -6,6 +6,8 @@ the flat parameter buffer (`ba3c_apply_update`), optionally with clip_by_average
 in (single replica).  SyncReplicasOptimizer replaces the parameter-server accumulators with
 an RCCL all-reduce of the flat clipped-gradient buffer (torch.distributed 'nccl' == RCCL).
 """
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -188,22 +190,47 @@ class SyncReplicasOptimizer(object):
     """tf.train.SyncReplicasOptimizer(opt, replicas_to_aggregate, total_num_replicas)
     (train.py:598-606) on one node: every rank clips its own gradients, the flat buffer is
     summed over RCCL (one all-reduce of 1.3-3.8 MB), and every rank applies the same update
-    with grad_scale = 1/N, so replicas stay bit-identical.  Backup workers / stale-gradient
-    dropping (num_grad < n_workers) have no synchronous single-node equivalent: the
-    aggregation is always over all `total_num_replicas` ranks (documented deviation)."""
+    with grad_scale = 1/N, so replicas stay bit-identical.
 
-    def __init__(self, opt, replicas_to_aggregate=None, total_num_replicas=None, group=None):
+    Backup workers (`replicas_to_aggregate` k < `total_num_replicas` N, the reference's
+    `--num_grad` below the worker count, train.py:601-602): TF's accumulator averages the
+    first k gradients that arrive for the current global step and drops the late ones as
+    stale (their local_step is behind once the chief has applied).  Here each step's arrival
+    order is the order in which the ranks' clipped gradients became ready on the device
+    (host CLOCK_MONOTONIC after a stream synchronise, shared by every process on the node,
+    exchanged with one all-gather of N doubles); the first k (ties: lower rank) contribute,
+    the others contribute zeros to the same all-reduce, and every rank applies the mean over
+    exactly k (grad_scale = 1/k).  All ranks then continue from the new parameters, as a
+    late TF worker does after dequeuing its next token.  Differences, documented: the
+    collective still waits for the stragglers (a synchronous all-reduce has no early exit,
+    so backup workers change the arithmetic, not the step time), and the mean is over
+    exactly k where TF's take_grad may average more that arrived before it ran."""
+
+    def __init__(self, opt, replicas_to_aggregate=None, total_num_replicas=None, group=None,
+                 arrival_fn=None):
         self._opt = opt
         self.group = group
         self.distributed = dist.is_available() and dist.is_initialized()
         world = dist.get_world_size(group) if self.distributed else 1
         self.total_num_replicas = total_num_replicas or world
         self.replicas_to_aggregate = replicas_to_aggregate or self.total_num_replicas
-        if self.total_num_replicas != world or self.replicas_to_aggregate != world:
-            raise ValueError("synchronous all-reduce aggregates exactly world_size=%d replicas "
-                             "(got replicas_to_aggregate=%s, total_num_replicas=%s)"
-                             % (world, replicas_to_aggregate, total_num_replicas))
+        if self.total_num_replicas != world:
+            raise ValueError("every rank of the group is one replica: total_num_replicas must "
+                             "be world_size=%d (got %s)" % (world, total_num_replicas))
+        if not 1 <= self.replicas_to_aggregate <= world:
+            raise ValueError("replicas_to_aggregate must be in [1, %d] (got %s)"
+                             % (world, replicas_to_aggregate))
         self.world = world
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        # arrival_fn(rank, step) -> float: a fixed arrival order for tests; None measures it
+        self.arrival_fn = arrival_fn
+        self.local_step = 0
+        self.last_aggregated = list(range(world))
+        self.dropped = 0                      # this rank's gradients dropped as stale
+
+    @property
+    def backup_workers(self):
+        return self.world - self.replicas_to_aggregate
 
     @property
     def learning_rate(self):
@@ -253,7 +280,14 @@ class SyncReplicasOptimizer(object):
 
     def allreduce(self, engine):
         """Sum of the replicas' flat gradient buffers over RCCL ('nccl' backend), issued on the
-        current HIP stream; runs whenever a process group exists (also at world size 1)."""
+        current HIP stream; runs whenever a process group exists (also at world size 1).  With
+        backup workers only the first k ranks' buffers enter the sum (select_first)."""
+        if self.distributed and self.backup_workers:
+            self.last_aggregated = self.select_first(engine)
+            if self.rank not in self.last_aggregated:
+                engine.grads.zero_()          # stale: dropped, as TF's accumulator does
+                self.dropped += 1
+        self.local_step += 1
         if self.distributed:
             self._all_reduce(engine.grads)
 
@@ -261,6 +295,24 @@ class SyncReplicasOptimizer(object):
         """Per-replica clip (multigpu.py:157) then the RCCL sum of the clipped buffer."""
         engine.clip_grads()
         self.allreduce(engine)
+
+    def _arrival(self, engine):
+        if self.arrival_fn is not None:
+            return float(self.arrival_fn(self.rank, self.local_step))
+        if engine.grads.is_cuda:
+            torch.cuda.current_stream(engine.grads.device).synchronize()
+        return time.monotonic()
+
+    def select_first(self, engine):
+        """Ranks whose gradients this step aggregates: the first k to arrive (one all-gather
+        of every rank's arrival time; ties go to the lower rank).  Returns the sorted list."""
+        t = torch.tensor([self._arrival(engine)], dtype=torch.float64)
+        if dist.get_backend(self.group) != "gloo":
+            t = t.to(engine.grads.device)
+        times = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(times, t, group=self.group)
+        order = sorted(range(self.world), key=lambda r: (float(times[r][0]), r))
+        return sorted(order[:self.replicas_to_aggregate])
 
     # bucketed exchange (SURVEY.md §8e): the fc1 + heads tensors (~90 % of the parameters at
     # F=512) are final after the first half of the backward pass, so their clip and RCCL sum
@@ -276,4 +328,5 @@ class SyncReplicasOptimizer(object):
         return self._all_reduce(engine.grads[off0:off1], async_op=True)
 
     def apply_gradients(self, engine):
-        self._opt.apply_gradients(engine, grad_scale=1.0 / self.world, fuse_clip=False)
+        self._opt.apply_gradients(engine, grad_scale=1.0 / self.replicas_to_aggregate,
+                                  fuse_clip=False)

@@ -63,7 +63,9 @@ class Ba3cTrainer(object):
     def train_step(self, state, action, futurereward):
         """Device-side step with no host synchronisation (used by bench.py)."""
         opt = self.optimizer
-        if isinstance(opt, SyncReplicasOptimizer) and self._fused_clip and opt.bucketed:
+        # backup workers pick the first k ranks once the whole gradient is ready: flat path
+        if (isinstance(opt, SyncReplicasOptimizer) and self._fused_clip and opt.bucketed
+                and not opt.backup_workers):
             self._bucketed_sync_step(state, action, futurereward)
             self.global_step += 1
             return
@@ -114,6 +116,9 @@ class Ba3cTrainer(object):
         undone: parameters, optimizer slots and beta powers are restored afterwards, so
         capturing does not train the model."""
         opt = self.optimizer
+        if isinstance(opt, SyncReplicasOptimizer) and opt.backup_workers:
+            raise ValueError("backup workers choose the aggregated ranks on the host each "
+                             "step; such a step cannot be captured as a graph")
         inner = opt._opt if isinstance(opt, SyncReplicasOptimizer) else opt
         if hasattr(inner, "use_device_state"):
             inner.use_device_state(self.engine.device)

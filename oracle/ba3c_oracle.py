@@ -549,10 +549,15 @@ def sample_from_u(probs, u):
 
 # --- full train step (trainer.py:244-299 -> one sess.run of TfDictOp) ---------------------
 def train_step(params, slots, step_t, batches, cfg, opt="adam", lr=1e-3, beta1=0.8,
-               beta2=0.75, eps=1e-8, entropy_beta=0.01):
+               beta2=0.75, eps=1e-8, entropy_beta=0.01, aggregate=None):
     """forward+backward per replica -> per-replica clip -> mean -> one optimizer apply.
 
     `batches` is a list of (state, action, R) per replica (1 entry = single worker).
+    `aggregate`: indices of the replicas whose clipped grads enter the mean (backup workers,
+    SyncReplicasOptimizer replicas_to_aggregate < total_num_replicas, train.py:601-602: the
+    accumulator of TF 1.2's sync_replicas_optimizer.py — not vendored in the reference —
+    averages the first replicas_to_aggregate fresh gradients and drops the stale rest);
+    None = all replicas.
     `slots` holds optimizer state; beta powers follow TF's float32 variables.
     Returns (new_params, new_slots, scalars of replica 0, clipped-mean grads).
     """
@@ -563,6 +568,8 @@ def train_step(params, slots, step_t, batches, cfg, opt="adam", lr=1e-3, beta1=0
         per.append({k: clip_by_average_norm(v) for k, v in g.items()})
         if sc0 is None:
             sc0 = sc
+    if aggregate is not None:
+        per = [per[i] for i in aggregate]
     g = per[0] if len(per) == 1 else sync_replicas_mean(per)
     newp, news = {}, {k: dict(v) if isinstance(v, dict) else v for k, v in slots.items()}
     f32 = np.float32

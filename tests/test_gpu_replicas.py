@@ -9,7 +9,10 @@ clip of each bucket (ba3c_clip_grads_range), the asynchronous bucket all-reduce 
 conv backward (trainer.py _bucketed_sync_step), the grad_scale = 1/N update, and rank 0's
 variables broadcast at start.  Checked: the replicas stay bit-identical, equal a one-process
 emulation (sum of the two clipped buffers, one apply) bit for bit, and the oracle's
-SyncReplicas step within the north-star tolerance.
+SyncReplicas step within the north-star tolerance.  The backup-worker case (num_grad=1 of 2,
+train.py:601-602) runs the same replicas with a fixed arrival order: each step only the first
+replica's clipped gradients enter the exchange and the update is bit-identical to applying
+that replica's buffer alone.
 """
 import os
 import socket
@@ -42,7 +45,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, bucketed, out):
+# backup-worker case: the rank whose gradients arrive first at each step
+FIRST = [1, 0]
+
+
+def _arrival(rank, step):
+    return 0.0 if rank == FIRST[step] else 1.0
+
+
+def _worker(rank, world, port, bucketed, out, k=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (root, os.path.join(root, "distributed-ba3c_amd")):
@@ -60,7 +71,8 @@ def _worker(rank, world, port, bucketed, out):
         # different initial variables per rank: the trainer broadcasts rank 0's
         m = Model(num_actions=A, fc_neurons=F, fc_splits=S, batch_size=B, max_batch=B, seed=20 + rank)
         own = m.engine.params.cpu().numpy()
-        opt = SyncReplicasOptimizer(AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), world, world)
+        opt = SyncReplicasOptimizer(AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), k or world, world,
+                                    arrival_fn=_arrival if k else None)
         opt.bucketed = bucketed
         tr = Ba3cTrainer(TrainConfig(model=m, optimizer=opt))
         p0 = m.engine.params.cpu().numpy()
@@ -75,9 +87,10 @@ def _worker(rank, world, port, bucketed, out):
         dist.destroy_process_group()
 
 
-def _emulate(p0_flat):
+def _emulate(p0_flat, only_first=False):
     """One process, one engine: per replica train_grads + clip_grads, the sum, one
-    apply_update(grad_scale=1/2, fuse_clip=0) — what the exchange must amount to."""
+    apply_update(grad_scale=1/2, fuse_clip=0) — what the exchange must amount to (backup
+    workers: the first replica's buffer alone, grad_scale=1)."""
     from ba3c_amd.engine import Ba3cEngine
     from ba3c_amd.optimizer import AdamOptimizer
     eng = Ba3cEngine(num_actions=A, fc_neurons=F, fc_splits=S, max_batch=B)
@@ -86,13 +99,13 @@ def _emulate(p0_flat):
     ps = []
     for step in range(2):
         total = torch.zeros_like(eng.grads)
-        for rank in range(2):
+        for rank in ([FIRST[step]] if only_first else range(2)):
             s, a, r = (torch.from_numpy(x).cuda() for x in _batch(step, rank))
             eng.train_grads(s, a, r)
             eng.clip_grads()
             total += eng.grads
         eng.grads.copy_(total)
-        opt.apply_gradients(eng, grad_scale=0.5, fuse_clip=False)
+        opt.apply_gradients(eng, grad_scale=1.0 if only_first else 0.5, fuse_clip=False)
         ps.append(eng.params.cpu().numpy())
     return eng, ps
 
@@ -130,3 +143,19 @@ def test_two_hip_replicas_exchange_gradients(bucketed):
         mask = np.abs(g[k]) > 1e-4 * max(np.abs(g[k]).max(), 1e-30)
         if mask.any():
             assert rel(d_got[mask], d_ref[mask]) < GRAD_TOL, k
+
+
+def test_two_hip_replicas_backup_worker_drops_the_late_gradients():
+    world = 2
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    mp.start_processes(_worker, args=(world, _free_port(), True, out, 1), nprocs=world, join=True,
+                       start_method="spawn")
+    (_, p0a, pa), (_, _, pb) = out[0], out[1]
+    _, emu = _emulate(p0a, only_first=True)
+    _, both = _emulate(p0a)
+    for step in range(2):
+        np.testing.assert_array_equal(pa[step], pb[step])
+        np.testing.assert_array_equal(pa[step], emu[step])
+    assert not np.array_equal(pa[0], both[0])           # the dropped replica's gradients mattered

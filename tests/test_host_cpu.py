@@ -103,24 +103,49 @@ def _batch(seed, B=2):
             rs.randint(0, 4, size=B).astype(np.int64), rs.normal(size=B).astype(np.float32))
 
 
-def _worker(rank, world, port, out, bucketed=True):
+# fixed arrival order per step for the backup-worker tests: ORDERS[step] lists ranks, first first
+ORDERS = [[2, 0, 1], [1, 2, 0]]
+
+
+def _fixed_arrival(rank, step):
+    return float(ORDERS[step].index(rank))
+
+
+def _worker(rank, world, port, out, bucketed=True, k=None, fixed=False, straggler=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import time
     from ba3c_amd.model import Model
     from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
     from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
     params = O.init_params(16, 2, 4, seed=0, dtype=np.float32)
     eng = OracleEngine(params)
     model = Model(num_actions=4, fc_neurons=16, fc_splits=2, batch_size=2, engine=eng)
-    opt = SyncReplicasOptimizer(AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), world, world)
+    opt = SyncReplicasOptimizer(AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), k or world, world,
+                                arrival_fn=_fixed_arrival if fixed else None)
     opt.bucketed = bucketed
     tr = Ba3cTrainer(TrainConfig(model=model, optimizer=opt))
+    chosen = []
     for step in range(2):
         s, a, r = _batch(10 * step + rank)
+        if straggler is not None and rank == straggler:
+            time.sleep(1.5)                   # this replica's gradients arrive last
         tr.train_step(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(r))
-    out[rank] = eng.params.numpy().copy()
+        chosen.append(list(opt.last_aggregated))
+    out[rank] = (eng.params.numpy().copy(), chosen, opt.dropped)
     dist.destroy_process_group()
+
+
+def _oracle_sync(world, aggregate=None):
+    params = O.init_params(16, 2, 4, seed=0, dtype=np.float32)
+    slots = O.init_slots(params, "adam", 0.8, 0.75)
+    for step in range(2):
+        batches = [_batch(10 * step + r) for r in range(world)]
+        params, slots, _, _ = O.train_step(params, slots, step + 1, batches, CFG, lr=1e-3,
+                                           beta1=0.8, beta2=0.75, eps=1e-8,
+                                           aggregate=None if aggregate is None else aggregate[step])
+    return np.concatenate([params[k].reshape(-1) for k in params])
 
 
 def _free_port():
@@ -140,22 +165,52 @@ def test_sync_replicas_world2_gloo_matches_oracle_sync_step(bucketed):
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out, bucketed), nprocs=world, join=True)
     # replicas stay bit-identical
-    np.testing.assert_array_equal(out[0], out[1])
+    np.testing.assert_array_equal(out[0][0], out[1][0])
     # and equal the oracle's SyncReplicas step: mean of per-replica clipped grads, one Adam
-    params = O.init_params(16, 2, 4, seed=0, dtype=np.float32)
-    slots = O.init_slots(params, "adam", 0.8, 0.75)
-    for step in range(2):
-        batches = [_batch(10 * step + r) for r in range(world)]
-        params, slots, _, _ = O.train_step(params, slots, step + 1, batches, CFG, lr=1e-3,
-                                           beta1=0.8, beta2=0.75, eps=1e-8)
-    ref = np.concatenate([params[k].reshape(-1) for k in params])
-    np.testing.assert_allclose(out[0], ref, rtol=2e-6, atol=1e-9)
+    np.testing.assert_allclose(out[0][0], _oracle_sync(world), rtol=2e-6, atol=1e-9)
 
 
-def test_sync_replicas_rejects_backup_workers():
+def test_backup_workers_aggregate_first_k_in_fixed_arrival_order():
+    """num_grad=2 of 3 workers (train.py:601-602): each step the two first-arriving replicas'
+    clipped grads are averaged, the third is dropped as stale; all replicas apply the same
+    update and equal the oracle's mean over that subset."""
+    world, k = 3, 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out, True, k, True), nprocs=world, join=True)
+    want = [sorted(o[:k]) for o in ORDERS]
+    for r in range(world):
+        np.testing.assert_array_equal(out[r][0], out[0][0])
+        assert out[r][1] == want
+        assert out[r][2] == sum(r not in w for w in want)
+    np.testing.assert_allclose(out[0][0], _oracle_sync(world, want), rtol=2e-6, atol=1e-9)
+    # dropping changes the update: the all-replica mean is a different point
+    assert np.abs(out[0][0] - _oracle_sync(world)).max() > 1e-7
+
+
+def test_backup_workers_drop_a_measured_straggler():
+    """Measured arrival (host monotonic clock after the gradients are ready): a replica that
+    sleeps 1.5 s before each step is the backup worker every step and its gradients never
+    enter the mean."""
+    world, k = 3, 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out, True, k, False, 1), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r][1] == [[0, 2], [0, 2]]
+        np.testing.assert_array_equal(out[r][0], out[0][0])
+    assert out[1][2] == 2
+    np.testing.assert_allclose(out[0][0], _oracle_sync(world, [[0, 2], [0, 2]]),
+                               rtol=2e-6, atol=1e-9)
+
+
+def test_sync_replicas_validates_replica_counts():
     from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
-    with pytest.raises(ValueError):
-        SyncReplicasOptimizer(AdamOptimizer(), replicas_to_aggregate=3, total_num_replicas=4)
+    with pytest.raises(ValueError):      # every rank is one replica: N must be the world size
+        SyncReplicasOptimizer(AdamOptimizer(), replicas_to_aggregate=1, total_num_replicas=4)
+    with pytest.raises(ValueError):      # cannot aggregate more replicas than exist
+        SyncReplicasOptimizer(AdamOptimizer(), replicas_to_aggregate=2, total_num_replicas=1)
+    assert SyncReplicasOptimizer(AdamOptimizer(), 1, 1).backup_workers == 0
 
 
 def test_adam_beta_powers_follow_tf_float32_variables():
