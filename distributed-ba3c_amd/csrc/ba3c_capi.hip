@@ -30,6 +30,23 @@
 
 using namespace ba3c;
 
+// The TfDictOp scalar reduction (scalars_block) as one workgroup of a multi-job launch: at
+// large batches it rides on conv3's weight-gradient launch instead of its own dependent
+// launch after the heads (nothing in the step reads the scalars).
+struct ScalarsJob {
+  struct Args {
+    const float* terms;
+    int B;
+    float beta;
+    const unsigned long long* relu;
+    double* out;
+  };
+  static constexpr int LDS = 0;
+  __device__ static void run(const Args& a, int, int, int, int, char*, uint32_t*) {
+    scalars_block(a.terms, a.B, a.beta, a.relu, a.out);
+  }
+};
+
 namespace {
 
 thread_local std::string g_err;
@@ -79,6 +96,11 @@ struct ba3c_handle {
   // gradient, (1) conv1's input gradient, or (0) runs alone (BA3C_C1PAIR)
   int c1pair = 2;
   uint32_t merged[BA3C_NUM_KERNELS] = {};   // ba3c_kernel_merged, per training pass
+  // large-batch scalar reduction deferred from run_heads onto conv3's weight-gradient launch
+  // (one-pass backward only; BA3C_SCALARS_RIDE=1; default: its own launch after the heads)
+  bool scalars_ride = false;
+  bool pend_scalars = false;
+  ScalarsJob::Args scalars_args{};
   bool w6w = true;    // conv1 weight gradient, B >= W6W_MIN_B: all channels per workgroup
                       // (BA3C_W6W=0: two 16-channel groups, wgrad6_kernel)
   // conv1 fwd / dgrad on the pipelined persistent band kernel (BA3C_PIPE=1).  Off: r02e
@@ -825,6 +847,12 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   } defer_guard(h);
   // join the side stream and run the deferred reductions of this phase in one launch
   auto finish = [&]() -> int {
+    if (h->pend_scalars) {     // no launch took the deferred scalar reduction
+      const ScalarsJob::Args& sa = h->scalars_args;
+      hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, sa.terms, sa.B, sa.beta, sa.relu, sa.out);
+      HIP_TRY(hipGetLastError());
+      h->pend_scalars = false;
+    }
     if (ws != s) {
       HIP_TRY(hipEventRecord(h->ev_join, ws));
       HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
@@ -918,7 +946,12 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
                           NoJob, true>(s, d, gd, g, gw, 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
       h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_CONV3_WGRAD;
     } else {
-      if (big) CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
+      const bool deep = (int)(gw.x * gw.y * gw.z) < h->cus;   // launch_gemm's ring depth
+      if (big && h->pend_scalars && h->g6 && !deep) {
+        CHECK((launch_multi<false, Gemm6Job<128, 64, 4, 1, decltype(g), 2>, ScalarsJob>(
+            ws, g, gw, h->scalars_args, dim3(1), 0, dim3(0, 1, 1), h, BA3C_K_CONV3_WGRAD)));
+        h->pend_scalars = false;
+      } else if (big) CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
       else CHECK((launch_gemm<128, 64, 4, 1, decltype(g), 2>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
       CHECK((launch_gemm<64, 64, 2, 2, decltype(d), 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
     }
@@ -1091,7 +1124,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
 
 int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, int B,
               const int64_t* action, const float* R, float beta, float explore, bool train,
-              float* probs, float* probsT, float* value, double* scalars = nullptr) {
+              float* probs, float* probsT, float* value, double* scalars = nullptr,
+              bool defer_scalars = false) {
   HeadsArgs a{};
   a.fcpart = w.fcpart;
   a.fc_split = FC_SPLIT;
@@ -1131,7 +1165,10 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
     hipLaunchKernelGGL(heads_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a);
   }
   HIP_TRY(hipGetLastError());
-  if (train && scalars && !fuse_scalars) {
+  if (train && scalars && !fuse_scalars && defer_scalars) {
+    h->scalars_args = ScalarsJob::Args{w.terms, B, beta, w.relu, scalars};
+    h->pend_scalars = true;      // launched by run_backward (conv3's weight gradient or finish)
+  } else if (train && scalars && !fuse_scalars) {
     hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, w.terms, B, beta, w.relu, scalars);
     HIP_TRY(hipGetLastError());
   }
@@ -1169,6 +1206,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
   if (const char* e = getenv("BA3C_W6W")) h->w6w = !(e[0] == '0');
   if (const char* e = getenv("BA3C_C1PAIR")) h->c1pair = e[0] - '0';
+  if (const char* e = getenv("BA3C_SCALARS_RIDE")) h->scalars_ride = e[0] != '0';
   if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
   if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
   if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 3;
@@ -1385,8 +1423,9 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
                                              : run_forward<12, 3>(h, s, params, state, batch, w, true));
   if (r != BA3C_OK) return r;
   // heads + loss + its gradient, fc1's split-K finish and (last workgroup) the TfDictOp scalars
+  h->pend_scalars = false;
   CHECK(run_heads(h, s, params, w, batch, action, futurereward, entropy_beta, 1.0f, true, nullptr,
-                  nullptr, nullptr, scalars));
+                  nullptr, nullptr, scalars, phase == 0 && h->scalars_ride && h->g6));
   if (h->cfg.channels == 4)
     return h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads, phase)
                       : run_backward<4, 3>(h, s, params, state, batch, w, grads, phase);

@@ -233,13 +233,16 @@ def test_greedy_eval_action_matches_numpy_argmax():
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
-def test_conv1_launch_pairings_match_default(monkeypatch, mode):
+@pytest.mark.parametrize("var,base,mode", [("BA3C_C1PAIR", None, "0"), ("BA3C_C1PAIR", None, "1"),
+                                           ("BA3C_SCALARS_RIDE", "0", "1")])
+def test_large_batch_launch_structures_match_default(monkeypatch, var, base, mode):
     """conv1's large-batch backward launch structure (BA3C_C1PAIR): 2 (default) = input gradient
     alone, then conv1's weight gradient beside conv0's in one launch; 1 = conv1 input + weight
     gradients in one launch; 0 = separate launches.  Every variant sums the same slabs in the
     same order (one per CU in the pair geometry), so the gradients, scalars and dP0 are
-    bit-identical — B=1024, 4 images per ring-walk workgroup."""
+    bit-identical — B=1024, 4 images per ring-walk workgroup.  BA3C_SCALARS_RIDE: the TfDictOp
+    scalar reduction in its own launch after the heads (0) or as one workgroup of conv3's
+    weight-gradient launch (1) — the same body, the same scalars."""
     B = 1024
     rs = np.random.RandomState(83)
     state = dev(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8))
@@ -247,11 +250,11 @@ def test_conv1_launch_pairings_match_default(monkeypatch, mode):
     R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
     params = O.init_params(512, 1, 4, seed=12, dtype=np.float32)
     out = []
-    for env in (None, mode):
+    for env in (base, mode):
         if env is None:
-            monkeypatch.delenv("BA3C_C1PAIR", raising=False)
+            monkeypatch.delenv(var, raising=False)
         else:
-            monkeypatch.setenv("BA3C_C1PAIR", env)
+            monkeypatch.setenv(var, env)
         eng = _engine(B)
         eng.load_params(params)
         sc = eng.train_grads(state, action, R)
