@@ -6,8 +6,13 @@ configs[2]/[3] — B=2048 per GPU, fc_neurons=512, fc_splits=1, A=4 (Breakout), 
 README's best hyper-parameters.  The B=32 / F=128 / S=4 parity configuration (configs[1]) is
 timed beside it.  Rank 0 prints ONE JSON line.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W     (N > 1: starts N rank processes itself)
     torchrun --nproc-per-node N ... bench.py --gpus N   (one process per GPU, RCCL)
+
+Without WORLD_SIZE in the environment and --gpus N > 1, this process is only a launcher: it
+makes no GPU call, starts N children (`python bench.py ...` with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, one per GPU), lets rank 0 print the
+line and exits with the worst child's status.
 """
 import argparse
 import json
@@ -77,7 +82,88 @@ def train_step_flops(B, C, F, A=4):
     return 2.0 * (fwd + fwd + (fwd - m["conv0"])) * B
 
 
-def build_trainer(B, F, S, A, world, seed):
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n, argv, script=None, grace=None):
+    """`python bench.py --gpus N` without torchrun: start N rank processes of `script` (this
+    file) with the environment torchrun would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), one per local GPU.  This
+    process makes no GPU call; the children inherit stdout (rank 0 prints the JSON line).
+    If a rank fails, the others get `grace` seconds (BA3C_SPAWN_GRACE, default 60) to end
+    before they are killed, so a dead peer cannot leave the job hanging in a collective.
+    Returns the worst exit status (a signal s counts as 128 + s)."""
+    import signal
+    import subprocess
+    if grace is None:
+        grace = float(os.environ.get("BA3C_SPAWN_GRACE", "60"))
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)]
+                                      + list(argv), env=env))
+
+    def stop(signum, frame):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, stop) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        failed_at = None
+        while True:
+            rcs = [p.poll() for p in procs]
+            if all(rc is not None for rc in rcs):
+                break
+            if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+                failed_at = time.time()
+            if failed_at is not None and time.time() - failed_at > grace:
+                for p in procs:
+                    if p.poll() is None:
+                        p.kill()
+            time.sleep(0.1)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return max(128 - rc if rc < 0 else rc for rc in rcs)
+
+
+def exchange_selftest(world, rank, iters=5):
+    """--exchange-selftest: the launcher and process group without a GPU — each rank sums a
+    gradient-sized fp32 buffer (0.95 M floats, F=512) over gloo on the CPU; rank 0 prints one
+    JSON line (CPU test of the spawner, tests/test_host_cpu.py)."""
+    dist.init_process_group("gloo")
+    n = 948229
+    x = torch.full((n,), float(rank + 1))
+    ts = []
+    for _ in range(iters):
+        x.fill_(float(rank + 1))
+        t0 = time.perf_counter()
+        dist.all_reduce(x)
+        ts.append(time.perf_counter() - t0)
+    ok = bool(torch.all(x == world * (world + 1) / 2.0))
+    el = torch.tensor([float(np.median(ts))], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "selftest": "gloo all-reduce of %d fp32 on the CPU"
+                          % n, "n_gpus": world, "sum_ok": ok,
+                          "allreduce_ms": round(float(el[0]) * 1000.0, 3)}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+def build_trainer(B, F, S, A, world, seed, sync=False):
     from ba3c_amd.model import Model
     from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
     from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
@@ -86,7 +172,8 @@ def build_trainer(B, F, S, A, world, seed):
     model = Model(num_actions=A, channels=1, fc_neurons=F, fc_splits=S, batch_size=B, max_batch=B,
                   seed=0)
     opt = AdamOptimizer(1e-3, beta1=0.8, beta2=0.75, epsilon=1e-8)   # README.md:35
-    if world > 1:
+    if world > 1 or sync:
+        # every rank's gradients enter every step's mean (no backup workers in the bench)
         opt = SyncReplicasOptimizer(opt, replicas_to_aggregate=world, total_num_replicas=world)
     tr = Ba3cTrainer(TrainConfig(model=model, optimizer=opt))
     g = torch.Generator(device="cuda").manual_seed(1000 + seed)
@@ -193,62 +280,100 @@ def overlap_bench(tr, batch, pred_batch, iters, world):
             "predict_states_per_s": round(world * pred_batch / (t_pred / 1000.0), 1)}
 
 
-def exchange_bench(tr, batch, iters, world, ms_step):
-    """N > 1: where the data-parallel exchange's time goes, per rank (max over ranks).
-    `local_step_ms` is the same bucketed step with the two RCCL sums left out (each rank clips
-    and applies its own gradients), `allreduce_ms` the two bucket sums run alone, so
-    `exposed_ms` = step - local is what the exchange adds to the step and `hidden_frac` how
-    much of the all-reduce time the conv backward covers (trainer.py:_bucketed_sync_step).
-    Runs after the timed region (replicas diverge while the exchange is off)."""
+# launches of the second backward phase, which run beside the fc1 + heads bucket's all-reduce
+PHASE2_KERNELS = ("conv3_dgrad", "conv3_wgrad", "conv2_dgrad", "conv1_dgrad", "conv0_wgrad",
+                  "wgrad_reduce")
+
+
+def exchange_report(tr, batch, timeline, iters, world):
+    """N > 1 (or --sync-path): where the data-parallel exchange's time goes.  `timeline` holds
+    the HIP events the timed steps recorded inside the real bucketed step (ExchangeTimeline:
+    phase 1, phase 2, each bucket's all-reduce from its clip to its end on the exchange
+    stream, the exposed wait, the update); every field is the max over ranks.  After the
+    timed region each phase-2 launch is probed over `iters` steps with the exchange running
+    and with it left out (each rank applies its own gradients; replicas diverge from here),
+    so the cost of RCCL sharing CUs with the persistent conv kernels shows per launch."""
     opt, eng = tr.optimizer, tr.engine
     tb, off = eng.bucket_split()
     total = eng.grads.numel()
+    tl = timeline.summary()
+    names = sorted(k for k in tl if k.endswith("_ms"))
 
-    def timed(fn):
-        sync_all(world)
-        t0 = time.perf_counter()
+    def probe(k):
+        eng.probe_enable(k)
         for _ in range(iters):
-            fn()
-        sync_all(world)
-        return (time.perf_counter() - t0) / iters * 1000.0
+            tr.train_step(*batch)
+        ms, n = eng.probe_read()
+        eng.probe_enable(None)
+        return ms / max(n, 1)
 
-    def ar(lo, hi):
-        w = opt._all_reduce(eng.grads[lo:hi], async_op=True)
-        if w is not None:
-            w.wait()
-
-    t_big = timed(lambda: ar(off, total))
-    t_small = timed(lambda: ar(0, off))
-    opt.distributed = False
+    tr.timeline = None
+    sync_all(world)
+    with_x = {k: probe(k) for k in PHASE2_KERNELS}
+    was, opt.distributed = opt.distributed, False
     try:
-        t_local = timed(lambda: tr.train_step(*batch))
+        local = {k: probe(k) for k in PHASE2_KERNELS}
     finally:
-        opt.distributed = True
-    el = torch.tensor([t_big, t_small, t_local], dtype=torch.float64, device="cuda")
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    t_big, t_small, t_local = (float(x) for x in el.tolist())
-    exposed = ms_step - t_local
-    return {"buckets": {"fc1_heads": {"bytes": 4 * (total - off), "allreduce_ms": round(t_big, 4)},
-                        "conv": {"bytes": 4 * off, "allreduce_ms": round(t_small, 4)}},
-            "backend": dist.get_backend(), "local_step_ms": round(t_local, 4),
-            "step_ms": round(ms_step, 4), "exposed_ms": round(exposed, 4),
-            "hidden_frac": round(1.0 - max(exposed, 0.0) / max(t_big + t_small, 1e-9), 3),
-            "iters": iters}
+        opt.distributed = was
+    vals = [tl[k] for k in names] + [with_x[k] for k in PHASE2_KERNELS] + \
+        [local[k] for k in PHASE2_KERNELS]
+    el = torch.tensor(vals, dtype=torch.float64, device="cuda")
+    if dist.is_initialized():
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = el.tolist()
+    tl.update({k: round(v, 4) for k, v in zip(names, el[:len(names)])})
+    n = len(PHASE2_KERNELS)
+    return {"buckets": {"fc1_heads": {"bytes": 4 * (total - off)}, "conv": {"bytes": 4 * off}},
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "timeline": tl,
+            "phase2_launch_ms": {k: {"with_exchange": round(a, 4), "exchange_off": round(b, 4)}
+                                 for k, a, b in zip(PHASE2_KERNELS, el[len(names):len(names) + n],
+                                                    el[len(names) + n:])},
+            "probe_iters": iters}
 
 
-def find_dominant_kernel(tr, batch):
+def find_dominant_kernel(tr, batch, steps=3):
+    """Probe every kernel id over `steps` steps: (the id with the longest launch time per
+    step, {id: ms per step}).  A multi-job launch is timed under its job 0's id; the other
+    jobs' ids read 0 (ba3c_kernel_merged lists them)."""
     from ba3c_amd._lib import KERNEL_IDS
     eng = tr.engine
     best, best_ms, per = None, -1.0, {}
     for name in KERNEL_IDS:
         eng.probe_enable(name)
-        tr.train_step(*batch)
+        for _ in range(steps):
+            tr.train_step(*batch)
         ms, n = eng.probe_read()
+        ms /= steps
         per[name] = ms
         if ms > best_ms:
             best, best_ms = name, ms
     eng.probe_enable(None)
     return best, per
+
+
+def step_ceiling(eng, per_kernel, B, C, F):
+    """The step against its real ceiling: every matrix launch's algorithmic FLOPs at the peak
+    of the arithmetic path it runs on (ba3c_kernel_split: fp16x3 838.9, u8 x fp16x2 1258,
+    bf16x6 419.4 TF/s), summed = the ideal step time of the mixed path; and the conv layers'
+    time-weighted fraction (ideal / measured over the conv0..conv3 launches, a multi-job
+    launch counted with all its jobs under job 0's time).  Elementwise / reduction launches
+    (heads, reductions, clip, update) are not in the ideal."""
+    macs = layer_macs(C, F)
+    ideal = {}
+    for k, layer in KERNEL_LAYER.items():
+        ideal[k] = 2.0 * macs[layer] * B / (kernel_peak(eng.kernel_split(k)) * 1e12) * 1e3
+    conv_ideal = conv_meas = 0.0
+    for k, ms in per_kernel.items():
+        if k not in KERNEL_LAYER or ms <= 0:
+            continue
+        jobs = [k] + [j for j in eng.kernel_merged(k) if j in KERNEL_LAYER]
+        if KERNEL_LAYER[k].startswith("conv"):
+            conv_ideal += sum(ideal[j] for j in jobs)
+            conv_meas += ms
+    return {"ideal_ms": round(sum(ideal.values()), 4),
+            "conv_ideal_ms": round(conv_ideal, 4), "conv_measured_ms": round(conv_meas, 4),
+            "conv_frac_time_weighted": round(conv_ideal / conv_meas, 4) if conv_meas else None}
 
 
 def cpu_threads():
@@ -327,41 +452,66 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one GPU per rank); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--sync-path", action="store_true",
+                    help="N=1: run the N>1 step (SyncReplicasOptimizer: phase-split backward, "
+                         "per-bucket clip, unfused update) in a world-1 RCCL group")
+    ap.add_argument("--exchange-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launcher only: no GPU call in this process (the children set their devices)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit("--gpus %d but WORLD_SIZE=%d (launch N>1 with torch.distributed.run)"
-                         % (args.gpus, world))
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.exchange_selftest:
+        sys.exit(exchange_selftest(world, rank))
+    sys.exit(run_rank(args, world, rank, local))
+
+
+def run_rank(args, world, rank, local):
+    from ba3c_amd.trainer import ExchangeTimeline
     if args.dist_backend == "gloo":
         # rehearsal of N ranks on fewer GPUs: the exchange goes through a host copy
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
-    if world > 1:
+    sync = world > 1 or args.sync_path
+    if sync:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
         if args.dist_backend == "gloo":
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
 
     B, F, S, A = args.batch, args.fc_neurons, args.fc_splits, args.num_actions
-    tr, batch = build_trainer(B, F, S, A, world, seed=rank)
+    C = 4
+    tr, batch = build_trainer(B, F, S, A, world, seed=rank, sync=sync)
     for _ in range(2):
         tr.train_step(*batch)
     sync_all(world)
     dom, per_kernel = find_dominant_kernel(tr, batch)
+    ceiling = step_ceiling(tr.engine, per_kernel, B, C, F)
     # A/B runs: time a named kernel over the timed steps instead of the dominant one
     dom = os.environ.get("BA3C_BENCH_PROBE", dom)
     sync_all(world)
 
+    timeline = None
+    if sync:
+        timeline = ExchangeTimeline()
+        tr.timeline = timeline          # events inside the real bucketed step
     elapsed, med_ms = time_steps(tr, batch, args.steps, args.warmup, world, probe=dom)
     probe_ms, launches = tr.engine.probe_read()
     tr.engine.probe_enable(None)
+    if timeline is not None:
+        # keep only the timed steps' events
+        timeline.steps = timeline.steps[-args.steps:]
 
     value = world * B * args.steps / elapsed
     ms_step = elapsed / args.steps * 1000.0
-    C = 4
     macs = layer_macs(C, F)
     dom_flops, dom_jobs = probe_flops(dom, tr.engine.kernel_merged(dom), macs, B)
     # a multi-job launch's ceiling: its total FLOPs over the time every job would take at the
@@ -393,6 +543,7 @@ def main():
                     "2516.6 TF dense 16-bit MFMA / %d split products" % split if len(dom_jobs) == 1 else
                     "total FLOPs / sum over jobs of (job FLOPs / 2516.6 TF x its split products)")}
     step_tflops = train_step_flops(B, C, F, A) / (ms_step / 1000.0) / 1e12
+    ceiling["step_frac_of_mixed_path_ceiling"] = round(ceiling["ideal_ms"] / ms_step, 4)
 
     out = {"metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
@@ -403,30 +554,33 @@ def main():
                    "reference initialisers (seed 0); resident in HBM",
            "config": {"workload": "configs[2]/[3]: BA3C train step (fwd+bwd+clip+%sAdam) "
                                   "B=%d/GPU, fc_neurons=%d, fc_splits=%d, A=%d"
-                                  % ("RCCL mean+" if world > 1 else "", B, F, S, A),
+                                  % ("RCCL mean+" if sync else "", B, F, S, A),
                       "global_batch": world * B, "per_gpu_batch": B, "fc_neurons": F,
-                      "fc_splits": S, "num_actions": A, "parallelism": "dp%d" % world},
+                      "fc_splits": S, "num_actions": A, "parallelism": "dp%d" % world,
+                      "step_path": "bucketed sync (phase-split backward, per-bucket clip, "
+                                   "unfused update)" if sync else "fused single replica",
+                      "backup_workers": 0},
            "step_tflops_algorithmic": round(step_tflops, 2),
-           "step_frac_of_bf16x6_peak": round(step_tflops / kernel_peak(6), 4),
            "step_vs_fp32_mfma_peak": round(step_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+           "ceiling": ceiling,
            "roofline": roof,
            "probe": {"kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": launches},
-           "kernel_ms_one_step": {k: round(v, 4) for k, v in per_kernel.items()}}
+           "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()}}
 
-    if world > 1:
-        out["exchange"] = exchange_bench(tr, batch, max(args.steps // 2, 5), world, ms_step)
+    if sync:
+        out["exchange"] = exchange_report(tr, batch, timeline, max(args.steps // 3, 5), world)
     if not args.no_overlap:
         out["overlap"] = overlap_bench(tr, batch, args.predict_batch, 10, world)
     if not args.no_b32:
         del tr
-        tr32, b32 = build_trainer(32, 128, 4, A, world, seed=rank)
+        tr32, b32 = build_trainer(32, 128, 4, A, world, seed=rank, sync=sync)
         n32 = max(args.steps, 100)
         el32, med32 = time_steps(tr32, b32, n32, 10, world)
         out["b32"] = {"config": "configs[1]: B=32/GPU, fc_neurons=128, fc_splits=4",
                       "value": round(world * 32 * n32 / el32, 1), "unit": "samples/s",
                       "ms_per_step": round(el32 / n32 * 1000.0, 4),
                       "ms_per_step_median": round(med32, 4), "launch": "eager"}
-        if world == 1:
+        if world == 1 and not sync:
             elg = time_graph_steps(tr32, b32, n32, 10)
             out["b32"].update({"value_graph": round(32 * n32 / elg, 1),
                                "ms_per_step_graph": round(elg / n32 * 1000.0, 4)})
@@ -435,9 +589,10 @@ def main():
         out["gpu_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if sync:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

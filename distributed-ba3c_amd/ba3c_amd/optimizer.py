@@ -6,6 +6,7 @@ the flat parameter buffer (`ba3c_apply_update`), optionally with clip_by_average
 in (single replica).  SyncReplicasOptimizer replaces the parameter-server accumulators with
 an RCCL all-reduce of the flat clipped-gradient buffer (torch.distributed 'nccl' == RCCL).
 """
+import os
 import time
 
 import numpy as np
@@ -175,14 +176,35 @@ def make_optimizer(name, lr, beta1=0.9, beta2=0.999, epsilon=1e-8):
 
 class _StagedWork(object):
     """Work handle of a host-staged all-reduce: wait() completes it and copies the sum back
-    into the device buffer (on the current stream, so later kernels see it)."""
+    into the device buffer (on `stream`, default the current one, so later kernels see it);
+    `end` (a timing event) is recorded on that stream after the copy."""
 
-    def __init__(self, work, host, dst):
+    def __init__(self, work, host, dst, stream=None, end=None):
         self.work, self.host, self.dst = work, host, dst
+        self.stream, self.end = stream, end
 
     def wait(self):
         self.work.wait()
-        self.dst.copy_(self.host)
+        if self.stream is None:
+            self.dst.copy_(self.host)
+            return True
+        with torch.cuda.stream(self.stream):
+            self.dst.copy_(self.host)
+            if self.end is not None:
+                self.end.record(self.stream)
+        torch.cuda.current_stream(self.dst.device).wait_stream(self.stream)
+        return True
+
+
+class _StreamJoin(object):
+    """Work handle of an all-reduce issued on the exchange stream: wait() makes the current
+    stream wait for it (no host synchronisation)."""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def wait(self):
+        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
         return True
 
 
@@ -224,6 +246,13 @@ class SyncReplicasOptimizer(object):
         self.rank = dist.get_rank(group) if self.distributed else 0
         # arrival_fn(rank, step) -> float: a fixed arrival order for tests; None measures it
         self.arrival_fn = arrival_fn
+        # measured arrivals compare CLOCK_MONOTONIC readings, which only one node shares
+        lws = os.environ.get("LOCAL_WORLD_SIZE")
+        if (world - self.replicas_to_aggregate) and arrival_fn is None and lws is not None \
+                and int(lws) != world:
+            raise ValueError("backup workers order arrivals by the node's monotonic clock: the "
+                             "group must be one node (LOCAL_WORLD_SIZE=%s, world size %d)"
+                             % (lws, world))
         self.local_step = 0
         self.last_aggregated = list(range(world))
         self.dropped = 0                      # this rank's gradients dropped as stale
@@ -318,14 +347,41 @@ class SyncReplicasOptimizer(object):
     # F=512) are final after the first half of the backward pass, so their clip and RCCL sum
     # run beside the conv layers' backward; the conv bucket follows at the end of the pass
     bucketed = True
+    _comm = None
 
-    def aggregate_bucket_async(self, engine, t0, t1, off0, off1):
+    def comm_stream(self, device):
+        """The exchange stream of the bucketed step: each bucket's sum is issued on it after
+        the bucket's clip, so its start and end can be marked with HIP events in the same
+        stream order as the collective (torch's NCCL stream joins it on wait())."""
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=device)
+        return self._comm
+
+    def aggregate_bucket_async(self, engine, t0, t1, off0, off1, marks=None):
         """Clip tensors [t0, t1) and start the RCCL sum of flat range [off0, off1) on the
-        process group's stream; returns the work handle (None without a process group)."""
+        exchange stream; returns the work handle (None without a process group).  `marks`:
+        (begin, end) timing events recorded on the exchange stream around the sum."""
         engine.clip_grads_range(t0, t1)
         if not self.distributed:
             return None
-        return self._all_reduce(engine.grads[off0:off1], async_op=True)
+        buf = engine.grads[off0:off1]
+        if not buf.is_cuda:
+            return self._all_reduce(buf, async_op=True)
+        comm = self.comm_stream(buf.device)
+        comm.wait_stream(torch.cuda.current_stream(buf.device))
+        begin, end = marks if marks is not None else (None, None)
+        with torch.cuda.stream(comm):
+            if begin is not None:
+                begin.record(comm)
+            if self._staged(buf):
+                host = buf.cpu()              # host-staged (gloo): waits for the clip
+                work = dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                return _StagedWork(work, host, buf, stream=comm, end=end)
+            work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            work.wait()                       # RCCL: `comm` waits for the collective's stream
+            if end is not None:
+                end.record(comm)
+        return _StreamJoin(comm)
 
     def apply_gradients(self, engine):
         self._opt.apply_gradients(engine, grad_scale=1.0 / self.replicas_to_aggregate,

@@ -49,14 +49,16 @@ def optimizer_config(args):
 
 
 def check_distributed(args, world):
-    """Synchronous data parallelism only: --use_sync with --ngrads == world size (backup
-    workers / stale-gradient dropping and the asynchronous PS mode have no single-node
-    all-reduce equivalent)."""
+    """Synchronous data parallelism only (the asynchronous PS mode has no all-reduce
+    equivalent): --use_sync with 1 <= --ngrads <= world size.  --ngrads below the world size
+    keeps the reference's backup workers (train.py:601-602): each step averages the first
+    `ngrads` ranks' gradients and drops the rest as stale (SyncReplicasOptimizer)."""
     if world > 1 and not args.use_sync:
         raise SystemExit("world size %d: multi-GPU training is synchronous (RCCL all-reduce); "
                          "pass --use_sync -g %d" % (world, world))
-    if args.use_sync and args.ngrads != world:
-        raise SystemExit("--ngrads %d must equal the number of GPU processes (%d)" % (args.ngrads, world))
+    if args.use_sync and not 1 <= args.ngrads <= world:
+        raise SystemExit("--ngrads %d must be in [1, %d] (the number of GPU processes)"
+                         % (args.ngrads, world))
 
 
 def build(args, rank=0, world=1, device=None):

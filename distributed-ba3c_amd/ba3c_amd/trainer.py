@@ -29,6 +29,42 @@ class TrainConfig(object):
         self.extra_arg = extra_arg or {}
 
 
+class ExchangeTimeline(object):
+    """HIP timing events of the bucketed data-parallel step (Ba3cTrainer._bucketed_sync_step),
+    recorded inside the real step: on the learner stream `start`, `fc1_ready` (phase 1 + the
+    fc1/heads bucket's clip done), `conv_ready` (phase 2 + the conv bucket's clip done),
+    `exchanged` (both sums joined) and `end` (update applied); on the exchange stream each
+    bucket's all-reduce begin / end.  summary() averages the intervals over the steps."""
+
+    MAIN = ("start", "fc1_ready", "conv_ready", "exchanged", "end")
+    COMM = ("fc1_ar_begin", "fc1_ar_end", "conv_ar_begin", "conv_ar_end")
+
+    def __init__(self):
+        self.steps = []
+
+    def new_step(self):
+        ev = {k: torch.cuda.Event(enable_timing=True) for k in self.MAIN + self.COMM}
+        self.steps.append(ev)
+        return ev
+
+    def summary(self):
+        """Mean milliseconds of each interval (call after the device has synchronised)."""
+        if not self.steps:
+            return None
+        keys = {"phase1_ms": ("start", "fc1_ready"), "phase2_ms": ("fc1_ready", "conv_ready"),
+                "fc1_allreduce_ms": ("fc1_ar_begin", "fc1_ar_end"),
+                "conv_allreduce_ms": ("conv_ar_begin", "conv_ar_end"),
+                "exposed_ms": ("conv_ready", "exchanged"), "update_ms": ("exchanged", "end"),
+                "step_ms": ("start", "end"),
+                # > 0: the fc1 + heads sum outlasted the conv backward by this much
+                "fc1_allreduce_tail_ms": ("conv_ready", "fc1_ar_end")}
+        out = {}
+        for name, (a, b) in keys.items():
+            out[name] = round(float(np.mean([s[a].elapsed_time(s[b]) for s in self.steps])), 4)
+        out["steps"] = len(self.steps)
+        return out
+
+
 class Ba3cTrainer(object):
     def __init__(self, config):
         self.config = config
@@ -61,7 +97,10 @@ class Ba3cTrainer(object):
                                "BA3C_FUSED_UPDATE=0" % (f, self.global_step))
 
     def train_step(self, state, action, futurereward):
-        """Device-side step with no host synchronisation (used by bench.py)."""
+        """Device-side step (used by bench.py).  No host synchronisation, except with backup
+        workers (SyncReplicasOptimizer with replicas_to_aggregate < world): each step then
+        synchronises the stream and all-gathers the ranks' ready times on the host before a
+        flat (not bucketed) all-reduce, so its step times are not comparable with k = N."""
         opt = self.optimizer
         # backup workers pick the first k ranks once the whole gradient is ready: flat path
         if (isinstance(opt, SyncReplicasOptimizer) and self._fused_clip and opt.bucketed
@@ -88,24 +127,37 @@ class Ba3cTrainer(object):
         """Data-parallel step with the gradient exchange in two buckets: phase 1 of the pass
         (forward, loss, heads + fc1 backward) -> clip + async RCCL sum of the fc1 + heads
         bucket -> phase 2 (conv backward, overlapping that all-reduce) -> clip + RCCL sum of
-        the conv bucket -> wait -> the identical update on every rank (grad_scale = 1/N)."""
+        the conv bucket -> wait -> the identical update on every rank (grad_scale = 1/N).
+        With a `timeline` attached (ExchangeTimeline, bench.py) the step records HIP events
+        at each of these points."""
         eng, opt, m = self.engine, self.optimizer, self.model
         tb, off = eng.bucket_split()
         nt, total = len(eng.layout), eng.grads.numel()
         inputs = [state, action, futurereward]
+        tl = self.timeline.new_step() if self.timeline is not None else None
+        mark = (lambda k: tl[k].record()) if tl is not None else (lambda k: None)
+        mark("start")
         m.train_phase = 1
         try:
             m.build_graph(inputs)
-            work = opt.aggregate_bucket_async(eng, tb, nt, off, total)
+            work = opt.aggregate_bucket_async(eng, tb, nt, off, total,
+                                              marks=tl and (tl["fc1_ar_begin"], tl["fc1_ar_end"]))
+            mark("fc1_ready")     # after the bucket's clip (the sum may start from here)
             m.train_phase = 2
             m.build_graph(inputs)
         finally:
             m.train_phase = 0
-        work2 = opt.aggregate_bucket_async(eng, 0, tb, 0, off)
+        work2 = opt.aggregate_bucket_async(eng, 0, tb, 0, off,
+                                           marks=tl and (tl["conv_ar_begin"], tl["conv_ar_end"]))
+        mark("conv_ready")
         for w in (work, work2):
             if w is not None:
                 w.wait()
+        mark("exchanged")
         opt.apply_gradients(eng)
+        mark("end")
+
+    timeline = None
 
     def capture_step(self, state, action, futurereward, warmup=2):
         """Capture one full step (fwd+bwd+clip+update) on static input tensors as a hipGraph

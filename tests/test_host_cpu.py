@@ -258,8 +258,12 @@ def test_launcher_flags_build_the_reference_configuration():
                                    replace_with_conv=True, ps=4, batch_size=32)
     assert optimizer_config(a) == dict(name="adam", lr=0.001, beta1=0.8, beta2=0.75, epsilon=1e-8)
     check_distributed(a, 2)
+    check_distributed(a, 4)                  # -g 2 of 4: two backup workers (train.py:601-602)
     with pytest.raises(SystemExit):
-        check_distributed(a, 4)              # --ngrads must equal the GPU process count
+        check_distributed(a, 1)              # cannot aggregate more gradients than processes
+    a.ngrads = 0
+    with pytest.raises(SystemExit):
+        check_distributed(a, 4)
     b = resolve(build_parser().parse_args("-b 32 -o rms".split()))
     check_distributed(b, 1)
     with pytest.raises(SystemExit):
@@ -282,3 +286,48 @@ def test_bench_prices_multi_job_launches_with_all_their_jobs():
     t = 2.0 * macs["conv0"] * B / (bench.kernel_peak(2) * 1e12) + \
         2.0 * macs["conv1"] * B / (bench.kernel_peak(3) * 1e12)
     assert abs(f / t / 1e12 - 961.2) < 0.5          # the r03b line's combined peak
+
+
+def _last_json(out):
+    import json
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_its_own_ranks_without_torchrun():
+    """`python bench.py --gpus 2` with no WORLD_SIZE (the driver's invocation) starts two rank
+    processes itself — RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, a gloo group formed, the
+    gradient-sized all-reduce summed — and rank 0 prints the one JSON line."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--exchange-selftest"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["sum_ok"] is True
+
+
+def test_bench_spawner_returns_the_failing_rank_status(tmp_path):
+    """A rank that dies makes the launcher stop the others after the grace period (a dead peer
+    must not leave rank 0 waiting in a collective) and exit with the failing status."""
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "assert os.environ['WORLD_SIZE'] == '3' and os.environ['LOCAL_RANK'] == str(r)\n"
+                      "assert os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "if r == 1: sys.exit(3)\n"
+                      "time.sleep(0 if r == 2 else 600)\n")
+    import time
+    t0 = time.time()
+    rc = bench.spawn_ranks(3, [], script=str(script), grace=1.0)
+    assert rc == 128 + 9 or rc == 3, rc          # rank 0 killed (SIGKILL) after rank 1's 3
+    assert time.time() - t0 < 60
+    ok = tmp_path / "ok.py"
+    ok.write_text("import os; assert os.environ['WORLD_SIZE'] == '2'\n")
+    assert bench.spawn_ranks(2, [], script=str(ok), grace=1.0) == 0
