@@ -15,7 +15,7 @@ KERNEL_IDS = {
     "conv0_fwd": 0, "conv1_fwd": 1, "conv2_fwd": 2, "conv3_fwd": 3, "fc1_fwd": 4, "heads": 5,
     "fc1_dgrad": 6, "conv3_dgrad": 7, "conv2_dgrad": 8, "conv1_dgrad": 9, "head_wgrad": 10,
     "fc1_wgrad": 11, "conv3_wgrad": 12, "conv2_wgrad": 13, "conv1_wgrad": 14, "conv0_wgrad": 15,
-    "wgrad_reduce": 16, "clip": 17, "update": 18,
+    "wgrad_reduce": 16, "clip": 17, "update": 18, "scalars": 19,
 }
 
 

@@ -689,55 +689,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
     band6r_body<L, PRE_>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
 }
 
-// Pipelined persistent variant (NPH == 1 layouts): one 512-thread workgroup per CU walks
-// bands blockIdx.x, + gridDim.x, ...; waves 4..7 stage band i + 1 into one of two LDS
-// buffers while waves 0..3 run band i's MFMAs from the other, one barrier per band.  The
-// staging (global loads + split VALU + LDS stores) of the one-band kernel runs beside the
-// MFMA chain instead of before it.
-template <class L>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) conv_band6p_kernel(const Band6Args a) {
-  static_assert(L::NPH == 1, "pipelined band kernel: unphased layouts");
-  using O = Band6Ops<L>;
-  using G = typename L::G;
-  static_assert(2 * L::LDS_BYTES <= 160 * 1024, "two band buffers");
-  __shared__ uint4 lds4[2 * L::LDS_BYTES / 16];
-  char* buf0 = reinterpret_cast<char*>(lds4);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform role branch
-  const bool loader = wave >= 4;
-  const int nbands = a.batch * G::NBANDS;
-  const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
-  auto scale_of = [&](int img) { return L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0; };
-  unsigned long long pos = 0;
-  int band = blockIdx.x;
-  if (loader && band < nbands) {
-    int img, y0, rows_out;
-    O::band_geom(band, img, y0, rows_out);
-    O::template stage<4>(a, buf0, tid - 256, img, y0, rows_out, 0, exp2i(scale_of(img)));
-  }
-  __syncthreads();
-  for (int i = 0; band < nbands; band += gridDim.x, ++i) {
-    char* cur = buf0 + (i & 1) * L::LDS_BYTES;
-    if (loader) {
-      const int nxt = band + gridDim.x;
-      if (nxt < nbands) {
-        int img, y0, rows_out;
-        O::band_geom(nxt, img, y0, rows_out);
-        O::template stage<4>(a, buf0 + ((i + 1) & 1) * L::LDS_BYTES, tid - 256, img, y0, rows_out, 0,
-                             exp2i(scale_of(img)));
-      }
-    } else {
-      int img, y0, rows_out;
-      O::band_geom(band, img, y0, rows_out);
-      float omax = 0.f;
-      O::compute(a, cur, wave, lane, img, y0, rows_out, exp2i(-scale_of(img)), us2, pos, omax, [](int) {});
-      if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
-    }
-    __syncthreads();
-  }
-  if (!loader && G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
-}
-
 // One launch per step for all weight preparation on the split path: job y < njobs writes the
 // NS split planes of band-conv copy y straight from the parameters (no fp32 [N][K] copy and no
 // second pass), job y == njobs (when w0 is set) prepares conv0's MFMA B fragments.  With the
@@ -753,12 +704,10 @@ struct WPrep6Args {
   unsigned long long* relu;  // training: ReLU-count slots zeroed here (no separate memset)
   uint32_t* amax;          // max-|x| slots zeroed here (n_amax words; may be null)
   int n_amax;
-  int* wexp;               // [5]: weight scale exponents of jobs 0..3 and conv0 (NS = 2)
-  int c0lay;               // conv0 forward LDS layout (its K order: conv0_wtap)
+  int* wexp;               // [5]: weight scale exponents of jobs 0..3 and conv0
 };
 
 // (bx, by, gx): blockIdx.x, blockIdx.y, gridDim.x of a plain launch; red4: 4 floats of LDS
-template <int NS>
 __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by, int gx, float* red4) {
   const int y = by;
   if (y == 0) {
@@ -768,17 +717,14 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
       for (int i = bx * 256 + threadIdx.x; i < a.n_amax; i += gx * 256) a.amax[i] = 0u;
   }
   if (y == a.jobs.njobs) {
-    int k = 0;
-    if constexpr (NS == 2) {
-      k = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, red4)));
-      if (bx == 0 && threadIdx.x == 0) a.wexp[4] = k;
-    }
-    conv0s_wprep_one<NS>(a.w0, a.wb0, bx * 256 + threadIdx.x, k, a.c0lay);
+    const int k = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, red4)));
+    if (bx == 0 && threadIdx.x == 0) a.wexp[4] = k;
+    conv0s_wprep_one(a.w0, a.wb0, bx * 256 + threadIdx.x, k);
     return;
   }
   const WPrepJob& j = a.jobs.job[y];
   float sc = 1.f;
-  if constexpr (NS == 2) {
+  {
     // max |W| over the tensor (L2-resident): four independent float4 loads in flight per
     // thread (a single dependent chain was ~15 us of the B=32 step)
     const float4* w4 = reinterpret_cast<const float4*>(j.w);
@@ -805,7 +751,7 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
     if (bx == 0 && threadIdx.x == 0) a.wexp[y] = k;
     sc = exp2i(k);
   }
-  uint16_t* dst = a.wt6 + NS * (size_t)a.off[y];
+  uint16_t* dst = a.wt6 + 2 * (size_t)a.off[y];
   // destination d in the band kernels' MFMA B-fragment order [K / 32][N / 16][lane][8]: lane
   // (lq, li) holds column n = 16 nb + li, K = 32 k32 + 8 lq .. + 7 (Band6Ops::compute)
   const int K = j.KH * j.KW * (j.dgrad ? j.CO : j.CI);
@@ -815,25 +761,18 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
     const int k32 = rest / NB, nb = rest - k32 * NB;
     const int e = BA3C_WFRAG ? (nb * 16 + li) * K + k32 * 32 + lq * 8 + kk : d;
     const float v = wprep_value(j, e);
-    if constexpr (NS == 3) {
-      uint32_t hi, mid, lo;
-      split3(v, hi, mid, lo);
-      dst[d] = (uint16_t)hi;
-      dst[j.n + d] = (uint16_t)mid;
-      dst[2 * j.n + d] = (uint16_t)lo;
-    } else {
-      uint32_t hi, lo;
-      split2(v * sc, hi, lo);
-      dst[d] = (uint16_t)hi;
-      dst[j.n + d] = (uint16_t)lo;
-    }
+    uint32_t hi, lo;
+    split2(v * sc, hi, lo);
+    dst[d] = (uint16_t)hi;
+    dst[j.n + d] = (uint16_t)lo;
   }
 }
 
-template <int NS>
+#if BA3C_SHARED_KERNELS  // non-template kernel: emitted by ba3c_capi.hip only
 __global__ void __launch_bounds__(256) wprep6_kernel(const WPrep6Args a) {
   __shared__ float red4[4];
-  wprep6_body<NS>(a, blockIdx.x, blockIdx.y, gridDim.x, red4);
+  wprep6_body(a, blockIdx.x, blockIdx.y, gridDim.x, red4);
 }
+#endif
 
 }  // namespace ba3c

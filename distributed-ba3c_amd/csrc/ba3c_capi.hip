@@ -25,7 +25,6 @@
 #include "ba3c_rollout.h"
 #include "ba3c_small.h"
 #include "ba3c_split.h"
-#include "ba3c_wgrad.h"
 #include "ba3c_wgrad6.h"
 
 using namespace ba3c;
@@ -88,10 +87,10 @@ struct ba3c_handle {
   int idx_piW, idx_pib, idx_vW, idx_vb;
   int per, wstride;
   TensorTable table;
-  bool band = true;   // band-conv kernels for conv1/conv2 fwd+dgrad (BA3C_GENERIC=1: GEMM engine)
-  bool split = true;  // conv0 on exact bf16-split MFMA when C == 4 (BA3C_CONV0_F32=1: fp32 band)
-  bool b6 = true;     // conv1/conv2 fwd+dgrad on bf16x6 split MFMA (BA3C_BAND6=0: fp32 band)
-  bool w6 = true;     // conv1/conv2 weight gradients on bf16x6 split MFMA (BA3C_WGRAD6=0: fp32)
+  // split-MFMA kernels (band convolutions, conv0, weight gradients, the bf16x6 GEMM engine);
+  // BA3C_GENERIC=1: every convolution and GEMM on the fp32-MFMA GEMM engine instead (a
+  // parity configuration with exact fp32 products)
+  bool band = true;
   // large batches: conv1's weight gradient shares a launch with (2, default) conv0's weight
   // gradient, (1) conv1's input gradient, or (0) runs alone (BA3C_C1PAIR)
   int c1pair = 2;
@@ -101,24 +100,12 @@ struct ba3c_handle {
   bool scalars_ride = false;
   bool pend_scalars = false;
   ScalarsJob::Args scalars_args{};
-  bool w6w = true;    // conv1 weight gradient, B >= W6W_MIN_B: all channels per workgroup
-                      // (BA3C_W6W=0: two 16-channel groups, wgrad6_kernel)
-  // conv1 fwd / dgrad on the pipelined persistent band kernel (BA3C_PIPE=1).  Off: r02e
-  // measured it slower (conv1 fwd 0.41 -> 0.51 ms, dgrad 0.43 -> 0.47 ms) — one compute wave
-  // per SIMD exposes the LDS-read latency that two co-resident one-band workgroups hide.
-  bool pipe = false;
   // conv1 fwd / dgrad (multi-band layouts) as ring-walk persistent kernels at batches that
   // give every workgroup whole images (conv_band6r_kernel; BA3C_RING=0: one band per workgroup)
   bool ring = true;
   int cus = 256;      // compute units of the device (persistent grids)
-  int c0lay = 3;      // conv0 forward LDS layout (ba3c_split.h; BA3C_C0LAY=2: r02's pairing)
   bool g6 = true;     // implicit-GEMM launches (conv3, fc1, heads; C=12 conv0) on bf16x6 split
-                      // MFMA (ba3c_gemm6.h; BA3C_GEMM6=0 or BA3C_GENERIC=1: fp32 MFMA)
-  // split family of the split kernels: 2 = scaled fp16 hi/lo, 3 MFMAs per fp32 product
-  // (default); 3 = bf16 hi/mid/lo, 6 MFMAs (BA3C_SPLIT=bf16).  The fp16 family needs every
-  // producer of a split operand to publish its max, so it is used only when all split
-  // kernels are on (band, b6, w6, split).
-  int ns = 2;
+                      // MFMA (ba3c_gemm6.h; off with BA3C_GENERIC=1: fp32 MFMA)
   // backward weight gradients on a side stream (created on the first training call that is
   // not being captured): 0 never (BA3C_OVERLAP=0), 1 always (BA3C_OVERLAP=1), 2 (default) for
   // batches <= OVERLAP_B only.  Large batches: r01t/u measured +0.5% step throughput (561k vs
@@ -181,24 +168,9 @@ constexpr int OVERLAP_B = 128;   // default side-stream weight gradients up to t
 using GConv2DW = BandGeom<22, 22, 64, 32, 5, 5, 18, false, 1, 8, 4, 4, 7, 7, 14, 14>;
 using GConv2FS = BandGeom<18, 18, 32, 64, 5, 5, 2, true, 0, 4>;
 using GConv2DS = BandGeom<22, 22, 64, 32, 5, 5, 3, false, 1, 8, 4, 4, 7, 7, 14, 14>;
-template <int NS>
-struct Lay;
-template <>
-struct Lay<3> {
-  using C1F = Band6<GConv1F, 192, 32, 7, 0, 3>;
-  using C1FP = C1F;
-  using C2F = Band6<GConv2F, 192, 32, 7, 0, 3>;
-  using C1D = Band6<GConv1D, 224, 128, 5, 0, 3>;
-  using C2D = Band6<GConv2DW, 224, 128, 11, 32, 3>;
-  using C2FS = Band6<GConv2FS, 192, 32, 2, 0, 3>;
-  using C2DS = Band6<GConv2DS, 224, 128, 2, 32, 3>;
-  using W1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 224, 3>;
-  using W2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 192, 3>;
-};
-template <>
-struct Lay<2> {
+// split-kernel layouts (scaled fp16 hi/lo planes)
+struct Lay {
   using C1F = Band6<GConv1F, 160, 128, 7, 0, 2, true>;
-  using C1FP = Band6<GConv1F, 160, 128, 7, 0, 2, false>;   // pipelined: no spill without DBUF
   using C2F = Band6<GConv2F, 160, 64, 7, 0, 2>;
 #ifndef BA3C_C1D_TILE4
 #define BA3C_C1D_TILE4 1
@@ -218,11 +190,8 @@ struct Lay<2> {
   using W2 = Wg6Geom<18, 18, 32, 64, 14, 16, 32, 96, 160, 2>;
   using W1W = Wg6WGeom<40, 40, 32, 32, 4, 160, 160>;   // conv1, B >= W6W_MIN_B (76.8 KB LDS)
 };
-// weight-gradient band kernels (ba3c_wgrad.h) and their persistent grid sizes
-using GWg0 = WgGeom<84, 84, 4, 5, 5, 32, 4, true, 1>;
-using GWg1 = WgGeom<40, 40, 32, 5, 5, 32, 4, false, 1>;
-using GWg2 = WgGeom<18, 18, 32, 5, 5, 64, 7, false, 2>;
-constexpr int WG_P0 = 512, WG_P1 = 512, WG_P2 = 256;
+// persistent grid bound of conv1's partial slabs
+constexpr int WG_P1 = 512;
 constexpr int W6_P1 = 256, W6_P2 = 128;   // x (c-groups x o-groups) = 512 workgroups
 // conv1 weight-gradient workgroups: ~4 bands each, at least 64 (at B=32 one band per
 // workgroup made 256 partial slabs of 100 KB — 26 MB written and read back by the reduction
@@ -297,8 +266,7 @@ size_t max_partials0(const ba3c_handle* h, int B) {
   size_t mx = 0;
   const WgradPlan w = plan_wgrad(25 * h->cfg.channels, 32, B * 6400, 128, 32);
   mx = std::max(mx, (size_t)w.S * w.M * w.N);
-  mx = std::max(mx, (size_t)WG_P0 * GWg0::M * 32);
-  mx = std::max(mx, (size_t)WG_P0S * Conv0W<3>::M * 32);
+  mx = std::max(mx, (size_t)WG_P0S * Conv0W<2>::M * 32);
   return mx;
 }
 
@@ -313,10 +281,8 @@ PartialSizes partial_sizes(const ba3c_handle* h, int B) {
   p.heads = sz(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
   p.fc1 = sz(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
   p.conv3 = sz(plan_wgrad(576, 64, B * 25, 128, 64));
-  p.conv2 = std::max({sz(plan_wgrad(800, 64, B * 196, 128, 64)), (size_t)WG_P2 * GWg2::M * 64,
-                      (size_t)W6_P2 * Lay<3>::W2::M * Lay<3>::W2::COUT});
-  p.conv1 = std::max({sz(plan_wgrad(800, 32, B * 1296, 128, 32)), (size_t)WG_P1 * GWg1::M * 32,
-                      (size_t)W6_P1 * Lay<3>::W1::M * Lay<3>::W1::COUT});
+  p.conv2 = std::max(sz(plan_wgrad(800, 64, B * 196, 128, 64)), (size_t)W6_P2 * Lay::W2::M * Lay::W2::COUT);
+  p.conv1 = std::max(sz(plan_wgrad(800, 32, B * 1296, 128, 32)), (size_t)WG_P1 * Lay::W1::M * Lay::W1::COUT);
   return p;
 }
 
@@ -439,17 +405,6 @@ int launch_reduce(ba3c_handle* h, hipStream_t s, const float* part, int S, const
     if (_r != BA3C_OK) return _r; \
   } while (0)
 
-template <class G>
-int launch_band(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a) {
-  dim3 grid(a.batch * G::NBANDS);
-  {
-    ProbeScope ps(h, s, kid);
-    hipLaunchKernelGGL(conv_band_kernel<G>, grid, dim3(256), 0, s, a);
-  }
-  HIP_TRY(hipGetLastError());
-  return BA3C_OK;
-}
-
 // Split operands of a band-conv launch (fp16 family): the max slots of the staged map, the
 // weight job whose scale exponent applies, and the slots that receive max |out| (-1: none).
 struct SplitIO {
@@ -491,11 +446,11 @@ int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const type
   return BA3C_OK;
 }
 
-// LP: the layout of the pipelined persistent variant (conv_band6p_kernel), used when the
-// launch has >= 4 bands per CU
-template <class L, class LP = L>
+// band conv on split MFMA; `ringable`: a multi-band layout that may run as the ring-walk
+// persistent kernel (whole images per workgroup) at large batches
+template <class L>
 int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
-                 int wt_off, SplitIO io, bool pipelined = false) {
+                 int wt_off, SplitIO io, bool ringable = false) {
   const Band6Args b = band6_args<L>(h, a, w, wt_off, io);
   const int nbands = a.batch * L::G::NBANDS;
   {
@@ -503,17 +458,10 @@ int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, cons
     if constexpr (L::NPH == 1 && L::G::NBANDS > 1 && L::G::SROWS > L::G::RB) {
       // whole images per workgroup: only where they split (nearly) evenly over 2 x CUs
       const int pr = 2 * h->cus;
-      if (pipelined && h->ring && a.batch >= pr && (a.batch % pr == 0 || a.batch >= 8 * pr)) {
+      if (ringable && h->ring && a.batch >= pr && (a.batch % pr == 0 || a.batch >= 8 * pr)) {
         // (the forward keeps its double-buffered A fragments and no row prefetch: the
         // no-DBUF layout with the prefetch measured 0.36 -> 0.41 ms, r02ai)
         hipLaunchKernelGGL(conv_band6r_kernel<L>, dim3(2 * h->cus), dim3(256), 0, s, b);
-        HIP_TRY(hipGetLastError());
-        return BA3C_OK;
-      }
-    }
-    if constexpr (LP::NPH == 1 && 2 * LP::LDS_BYTES <= 160 * 1024) {
-      if (pipelined && h->pipe && nbands >= 4 * h->cus) {
-        hipLaunchKernelGGL(conv_band6p_kernel<LP>, dim3(std::min(nbands, h->cus)), dim3(512), 0, s, b);
         HIP_TRY(hipGetLastError());
         return BA3C_OK;
       }
@@ -522,35 +470,6 @@ int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, cons
   }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
-}
-
-// band conv: split MFMA when enabled, fp32 MFMA otherwise
-template <class L, class LP = L>
-int launch_bandx(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, const Workspace& w,
-                 int wt_off, SplitIO io, bool pipelined = false) {
-  if (h->b6) return launch_band6<L, LP>(h, s, kid, a, w, wt_off, io, pipelined);
-  return launch_band<typename L::G>(h, s, kid, a);
-}
-
-// persistent weight-gradient band kernel + deterministic reduction into the flat HWIO grads
-template <class G>
-int launch_wgband(ba3c_handle* h, hipStream_t s, int kid, const WgArgs& a, int pmax, float* dst,
-                  int cinpad) {
-  const int nbands = a.batch * G::NBANDS;
-  const int P = std::min(pmax, nbands);
-  {
-    ProbeScope ps(h, s, kid);
-    hipLaunchKernelGGL(wgrad_band_kernel<G>, dim3(P, G::NSPLIT), dim3(256), 0, s, a);
-  }
-  HIP_TRY(hipGetLastError());
-  ReduceMap mp{};
-  mp.kind = 0;
-  mp.M = G::M;
-  mp.N = G::COUT;
-  mp.cin = G::CIN;
-  mp.cinpad = cinpad;
-  mp.dst = dst;
-  return launch_reduce(h, s, a.part, P, mp);
 }
 
 // split weight-gradient kernel + deterministic reduction into the flat HWIO grads
@@ -603,14 +522,12 @@ WPrep6Args wprep6_args(ba3c_handle* h, const float* prm, const Workspace& w, boo
   pa.amax = w.amax;
   pa.n_amax = AMAX_N * (1 + h->cfg.max_batch);
   pa.wexp = w.wexp;
-  pa.c0lay = h->c0lay;
   return pa;
 }
 
 // Small batches (split path, C == 4): the conv0 fragments + zeroing launch alone, then the
 // band-conv weight jobs run beside conv0's forward in one multi-job launch (they are only
 // needed from conv1 on).  B=32: the 8 us weight-prep launch was on the critical path.
-template <int NS>
 int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
                             const Workspace& w, bool train) {
   WPrep6Args first = wprep6_args(h, prm, w, train);
@@ -619,142 +536,83 @@ int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, con
   rest.w0 = nullptr;                    // rows 0..njobs-1 only, no zeroing: conv0 publishes
   rest.relu = nullptr;                  // into those counters concurrently
   rest.amax = nullptr;
-  hipLaunchKernelGGL(wprep6_kernel<NS>, dim3(64, 1), dim3(256), 0, s, first);
+  hipLaunchKernelGGL(wprep6_kernel, dim3(64, 1), dim3(256), 0, s, first);
   HIP_TRY(hipGetLastError());
   const Conv0SArgs sa{state, reinterpret_cast<const uint4*>(w.wt + WT_C0S), w.p0, train ? w.c0 : nullptr,
                       train ? w.relu : nullptr, B, w.wexp + 4, w.am(AM_P0, h)};
   ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-  return launch_multi<false, Conv0SJob<NS, 3>, WPrep6Job<NS>>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)),
-                                                              rest, dim3(64, rest.jobs.njobs));
+  return launch_multi<false, Conv0SJob, WPrep6Job>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)), rest,
+                                                  dim3(64, rest.jobs.njobs));
 }
 
-// [N][K] copies of the band-conv weights for this step (forward; + rotated dgrad in training)
-template <int NS>
+// split planes of the band-conv weights for this step (forward; + rotated dgrad in training)
+// and, for C == 4, conv0's MFMA B fragments: one launch
 int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, bool train) {
-  const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
-  const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
-  WPrepArgs a{};
-  a.job[0] = WPrepJob{W1, w.wt + WT_C1F, 5, 5, 32, 32, 0, 800 * 32};
-  a.job[1] = WPrepJob{W2, w.wt + WT_C2F, 5, 5, 32, 64, 0, 800 * 64};
-  a.job[2] = WPrepJob{W1, w.wt + WT_C1D, 5, 5, 32, 32, 1, 800 * 32};
-  a.job[3] = WPrepJob{W2, w.wt + WT_C2D, 5, 5, 32, 64, 1, 1600 * 32};
-  a.njobs = train ? 4 : 2;
-  const bool c0s = h->cfg.channels == 4 && h->split;
-  if (h->b6) {
-    // split path: one launch writes the splits (and conv0's fragments) directly
-    WPrep6Args pa = wprep6_args(h, prm, w, train);
-    if (!c0s) pa.w0 = nullptr;
-    hipLaunchKernelGGL(wprep6_kernel<NS>, dim3(64, a.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
-    HIP_TRY(hipGetLastError());
-  } else {
-    hipLaunchKernelGGL(wprep_kernel, dim3(64, a.njobs), dim3(256), 0, s, a);
-    HIP_TRY(hipGetLastError());
-  }
-  if (c0s) {
-    if (!h->b6) {
-      hipLaunchKernelGGL(conv0s_wprep_kernel, dim3((2 * Conv0S::KSTEPS * 64 + 255) / 256), dim3(256),
-                         0, s, prm + h->tensors[h->idx_conv[0]].offset,
-                         reinterpret_cast<uint4*>(w.wt + WT_C0S), h->c0lay);
-      HIP_TRY(hipGetLastError());
-    }
-  } else if (h->cfg.channels == 4) {
-    hipLaunchKernelGGL(conv0_wprep_kernel, dim3((32 * Conv0Geom::KDIM + 255) / 256), dim3(256), 0, s,
-                       prm + h->tensors[h->idx_conv[0]].offset, w.wt + WT_C0F);
-    HIP_TRY(hipGetLastError());
-  }
-  return BA3C_OK;
-}
-
-template <int NS>
-int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a, const Workspace& w) {
-  if (h->split) {
-    const Conv0SArgs sa{reinterpret_cast<const uint8_t*>(a.src),
-                        reinterpret_cast<const uint4*>(w.wt + WT_C0S), a.out, a.out_code,
-                        a.relu_count, a.batch, w.wexp + 4, w.am(AM_P0, h)};
-    ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-    const dim3 grid(std::min(FW_P0S, a.batch * Conv0S::NBANDS));
-    HIP_TRY(launch_conv0s_fwd(NS, h->c0lay, grid, s, sa));   // ba3c_conv0.hip
-  } else {
-    ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-    hipLaunchKernelGGL(conv0_band_kernel, dim3(a.batch * Conv0Geom::NBANDS), dim3(256), 0, s, a);
-  }
+  WPrep6Args pa = wprep6_args(h, prm, w, train);
+  const bool c0s = h->cfg.channels == 4;
+  if (!c0s) pa.w0 = nullptr;
+  hipLaunchKernelGGL(wprep6_kernel, dim3(64, pa.jobs.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
 
+int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a, const Workspace& w) {
+  const Conv0SArgs sa{reinterpret_cast<const uint8_t*>(a.src), reinterpret_cast<const uint4*>(w.wt + WT_C0S),
+                      a.out, a.out_code, a.relu_count, a.batch, w.wexp + 4, w.am(AM_P0, h)};
+  ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
+  const dim3 grid(std::min(FW_P0S, a.batch * Conv0S::NBANDS));
+  HIP_TRY(launch_conv0s_fwd(grid, s, sa));   // ba3c_conv0.hip
+  return BA3C_OK;
+}
+
 // ---- forward --------------------------------------------------------------------------
-// NS: split family of the split kernels (2 scaled fp16, 3 bf16); see ba3c_split.h.
-template <int CH, int NS>
+// Split kernels (h->band): conv0 (C == 4) and the conv1 / conv2 band convolutions on scaled
+// fp16 hi/lo MFMA (ba3c_split.h, ba3c_band6.h); C == 12's conv0, conv3 and fc1 on the bf16x6
+// GEMM engine.  BA3C_GENERIC=1: every layer on the fp32-MFMA GEMM engine.
+template <int CH>
 int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
                 const Workspace& w, bool train) {
-  using LY = Lay<NS>;
+  using LY = Lay;
   const int F = h->cfg.fc_neurons;
   const float* W0 = prm + h->tensors[h->idx_conv[0]].offset;
   const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
   const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3 = prm + h->tensors[h->idx_conv[3]].offset;
   unsigned long long* rc = train ? w.relu : nullptr;
-  uint32_t* am_p0 = NS == 2 ? w.am(AM_P0, h) : nullptr;
+  uint8_t* c0 = train ? w.c0 : nullptr;
+  uint8_t* c1 = train ? w.c1 : nullptr;
+  uint8_t* c2 = train ? w.c2 : nullptr;
   const SplitIO io1{AM_P0, 0, AM_P1}, io2{AM_P1, 1, -1};
-  // small batches on the split path: weight prep beside conv0's forward (one launch fewer on
-  // the critical path)
-  const bool mj = h->multi && B <= OVERLAP_B && CH == 4 && h->band && h->b6 && h->split && NS == 2 &&
-                  h->c0lay == 3;
-  if (mj) CHECK(launch_prep_conv0_multi<NS>(h, s, prm, state, B, w, train));
-  else if (h->band) CHECK(launch_wprep<NS>(h, s, prm, w, train));
-  if (train) {
+  if (!h->band) {
+    ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> cv0{state, W0, w.p0, c0, rc, 1.0f / 255.0f, B * 6400, 32, 25 * CH, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, cv0, 1)));
+    ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> cv1{w.p0, W1, w.p1, c1, rc, 1.0f, B * 1296, 32, 800, 0};
+    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, cv1, 1)));
+    ConvFwd<false, 18, 18, 32, 32, 5, 5, 64, 0> cv2{w.p1, W2, w.p2, c2, rc, 1.0f, B * 196, 64, 800, 0};
+    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, cv2, 1)));
+  } else {
+    // small batches: weight prep beside conv0's forward (one launch fewer on the critical path)
+    const bool mj = h->multi && B <= OVERLAP_B && CH == 4;
     if (mj) {
-      // conv0 ran beside the weight prep above
-    } else if (h->band && CH == 4) {
-      CHECK(launch_conv0_band<NS>(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
-                                                 w.wt + WT_C0F, w.p0, w.c0, rc, B}, w));
+      CHECK(launch_prep_conv0_multi(h, s, prm, state, B, w, train));
     } else {
-      ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> c0{state, W0, w.p0, w.c0, rc, 1.0f / 255.0f,
-                                                   B * 6400, 32, 25 * CH, 0, am_p0};
-      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
+      CHECK(launch_wprep(h, s, prm, w, train));
+      if constexpr (CH == 4) {
+        CHECK(launch_conv0_band(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr, nullptr, w.p0, c0,
+                                               rc, B}, w));
+      } else {
+        ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> cv0{state, W0, w.p0, c0, rc, 1.0f / 255.0f,
+                                                      B * 6400, 32, 25 * CH, 0, w.am(AM_P0, h)};
+        CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, cv0, 1)));
+      }
     }
-    if (h->band) {
-      CHECK((launch_bandx<typename LY::C1F, typename LY::C1FP>(h, s, BA3C_K_CONV1_FWD,
-                                          BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, w.c1, rc, B}, w,
-                                          WT_C1F, io1, true)));
-      const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, w.c2, rc, B};
-      if (h->b6 && B <= SMALL_B)
-        CHECK(launch_band6<typename LY::C2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
-      else
-        CHECK(launch_bandx<typename LY::C2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
-    } else {
-      ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 0> c1{w.p0, W1, w.p1, w.c1, rc, 1.0f, B * 1296, 32, 800, 0};
-      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
-      ConvFwd<false, 18, 18, 32, 32, 5, 5, 64, 0> c2{w.p1, W2, w.p2, w.c2, rc, 1.0f, B * 196, 64, 800, 0};
-      CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
-    }
-  } else if (h->band) {
-    if (mj) {
-      // conv0 ran beside the weight prep above
-    } else if (CH == 4) {
-      CHECK(launch_conv0_band<NS>(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr,
-                                                 w.wt + WT_C0F, w.p0, nullptr, nullptr, B}, w));
-    } else {
-      ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
-                                                   B * 6400, 32, 25 * CH, 0, am_p0};
-      CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
-    }
-    CHECK((launch_bandx<typename LY::C1F, typename LY::C1FP>(h, s, BA3C_K_CONV1_FWD,
-                                        BandArgs{w.p0, nullptr, w.wt + WT_C1F, w.p1, nullptr, nullptr, B}, w,
-                                        WT_C1F, io1, true)));
-    const BandArgs a2{w.p1, nullptr, w.wt + WT_C2F, w.p2, nullptr, nullptr, B};
-    if (h->b6 && B <= SMALL_B)
+    CHECK((launch_band6<typename LY::C1F>(h, s, BA3C_K_CONV1_FWD, BandArgs{w.p0, nullptr, nullptr, w.p1, c1, rc, B},
+                                          w, WT_C1F, io1, true)));
+    const BandArgs a2{w.p1, nullptr, nullptr, w.p2, c2, rc, B};
+    if (B <= SMALL_B)
       CHECK(launch_band6<typename LY::C2FS>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
     else
-      CHECK(launch_bandx<typename LY::C2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
-  } else {
-    ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 1> c0{state, W0, w.p0, nullptr, nullptr, 1.0f / 255.0f,
-                                                 B * 6400, 32, 25 * CH, 0};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, c0, 1)));
-    ConvFwd<false, 40, 40, 32, 32, 5, 5, 32, 1> c1{w.p0, W1, w.p1, nullptr, nullptr, 1.0f, B * 1296, 32, 800, 0};
-    CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_FWD, c1, 1)));
-    ConvFwd<false, 18, 18, 32, 32, 5, 5, 64, 1> c2{w.p1, W2, w.p2, nullptr, nullptr, 1.0f, B * 196, 64, 800, 0};
-    CHECK((launch_gemm<128, 64, 4, 1>(h, s, BA3C_K_CONV2_FWD, c2, 1)));
+      CHECK(launch_band6<typename LY::C2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
   }
   ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
   // K = 576 in two halves of 9 k-tiles summed in the workgroup (KS = 2) at every batch, so
@@ -799,10 +657,10 @@ int ensure_side_stream(ba3c_handle* h, hipStream_t s) {
 // reductions (those gradients are final when it returns); phase 2: conv3..conv0 and theirs.
 // Phases 1 + 2 compute exactly phase 0; between them a data-parallel caller can all-reduce
 // the fc1 + heads bucket (most of the parameters) while the conv layers run.
-template <int CH, int NS>
+template <int CH>
 int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* state, int B,
                  const Workspace& w, float* grads, int phase = 0) {
-  using LY = Lay<NS>;
+  using LY = Lay;
   const int F = h->cfg.fc_neurons, A = h->cfg.num_actions;
   const bool legacy = !h->cfg.replace_with_conv;
   const float* W1c = prm + h->tensors[h->idx_conv[1]].offset;
@@ -826,7 +684,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // small batches on the split path: each layer's input- and weight-gradient kernels as one
   // multi-job launch on `s` (no side stream, no events); otherwise the side stream joins a
   // graph capture of `s` through the fork events
-  const bool mjok = h->multi && h->overlap != 1 && h->band && h->b6 && h->w6 && h->g6 && h->split && CH == 4;
+  const bool mjok = h->multi && h->overlap != 1 && h->band && CH == 4;
   const bool mj = mjok && B <= OVERLAP_B;
   const bool mj_fc = mj || (mjok && (h->multi_big & 1));
   const bool mj_c2 = !mj && mjok && (h->multi_big & 2);   // large-batch conv2 pair (A/B: BA3C_MULTI_BIG=3)
@@ -849,6 +707,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   auto finish = [&]() -> int {
     if (h->pend_scalars) {     // no launch took the deferred scalar reduction
       const ScalarsJob::Args& sa = h->scalars_args;
+      ProbeScope ps(h, s, BA3C_K_SCALARS);
       hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, sa.terms, sa.B, sa.beta, sa.relu, sa.out);
       HIP_TRY(hipGetLastError());
       h->pend_scalars = false;
@@ -935,7 +794,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     WgradPlan pl = plan_wgrad(576, 64, B * 25, 128, 64);
     ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
     ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0,
-                                           NS == 2 ? w.am(AM_DP2, h) : nullptr};
+                                           h->band ? w.am(AM_DP2, h) : nullptr};
     // The input gradient splits its k-tiles over two wave groups of a 512-thread workgroup
     // (KS = 2) at every batch (each image's dP2 rounds the same in any batch, like the
     // forward); the weight gradient does for B <= OVERLAP_B (r02x: KS = 2 at B=2048 35 -> 45 us),
@@ -950,6 +809,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       if (big && h->pend_scalars && h->g6 && !deep) {
         CHECK((launch_multi<false, Gemm6Job<128, 64, 4, 1, decltype(g), 2>, ScalarsJob>(
             ws, g, gw, h->scalars_args, dim3(1), 0, dim3(0, 1, 1), h, BA3C_K_CONV3_WGRAD)));
+        h->merged[BA3C_K_CONV3_WGRAD] |= 1u << BA3C_K_SCALARS;   // the reduction rode on this launch
         h->pend_scalars = false;
       } else if (big) CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
       else CHECK((launch_gemm<128, 64, 4, 1, decltype(g), 2>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
@@ -978,13 +838,10 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     h->merged[BA3C_K_CONV2_DGRAD] |= 1u << BA3C_K_CONV2_WGRAD;
     CHECK(reduce_wgrad6<typename LY::W2>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[2]].offset));
   } else {
-    if (h->band && h->w6) {
+    if (h->band) {
       CHECK(launch_wgrad6<typename LY::W2>(h, ws, BA3C_K_CONV2_WGRAD,
                                           Wg6Args{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)},
                                           W6_P2, grads + h->tensors[h->idx_conv[2]].offset));
-    } else if (h->band) {
-      CHECK(launch_wgband<GWg2>(h, ws, BA3C_K_CONV2_WGRAD, WgArgs{w.p1, w.dp2, w.c2, w.part_2, B}, WG_P2,
-                                grads + h->tensors[h->idx_conv[2]].offset, 32));
     } else {
       WgradPlan pl = plan_wgrad(800, 64, B * 196, 128, 64);
       ConvWgrad<false, 18, 18, 32, 5, 5, 64, true> g{w.p1, w.dp2, w.c2, w.part_2, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
@@ -994,10 +851,10 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     if (h->band) {
       const BandArgs ba{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B};
       const SplitIO io{AM_DP2, 3, AM_DP1};
-      if (h->b6 && B <= SMALL_B)
+      if (B <= SMALL_B)
         CHECK(launch_band6<typename LY::C2DS>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D, io));
       else
-        CHECK(launch_bandx<typename LY::C2D>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D, io));
+        CHECK(launch_band6<typename LY::C2D>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D, io));
     } else {
       ConvDgrad<18, 18, 32, 5, 5, 64, true> d{w.dp2, w.c2, W2c, w.dp1, B * 324, 32, 1600, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV2_DGRAD, d, 1)));
@@ -1016,9 +873,9 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[1]].offset));
   } else {
     bool done = false, paired = false;
-    if constexpr (NS == 2) {
-      const bool pairgeo = h->band && h->b6 && h->w6 && h->w6w && h->ring && conv1_pair_geometry(B, h->cus);
-      if (pairgeo && h->c1pair == 2 && CH == 4 && h->split) {
+    {
+      const bool pairgeo = h->band && h->ring && conv1_pair_geometry(B, h->cus);
+      if (pairgeo && h->c1pair == 2 && CH == 4) {
         done = defer_w1 = true;                             // beside conv0's weight gradient below
       }
       // conv1 input and weight gradients in one launch, one workgroup of each per CU (each job
@@ -1034,7 +891,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
         CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, h->cus, grads + h->tensors[h->idx_conv[1]].offset));
         done = paired = true;
       }
-      if (!done && h->band && h->w6 && h->w6w && B >= W6W_MIN_B) {
+      if (!done && h->band && B >= W6W_MIN_B) {
         using GW = typename LY::W1W;
         const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
         const int P = conv1_w6w_p(B, h->cus);
@@ -1048,13 +905,10 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       }
     }
     if (done) {
-    } else if (h->band && h->w6) {
+    } else if (h->band) {
       CHECK(launch_wgrad6<typename LY::W1>(h, ws, BA3C_K_CONV1_WGRAD,
                                           Wg6Args{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)},
                                           conv1_wgrad_p(B), grads + h->tensors[h->idx_conv[1]].offset));
-    } else if (h->band) {
-      CHECK(launch_wgband<GWg1>(h, ws, BA3C_K_CONV1_WGRAD, WgArgs{w.p0, w.dp1, w.c1, w.part_1, B}, WG_P1,
-                                grads + h->tensors[h->idx_conv[1]].offset, 32));
     } else {
       WgradPlan pl = plan_wgrad(800, 32, B * 1296, 128, 32);
       ConvWgrad<false, 40, 40, 32, 5, 5, 32, true> g{w.p0, w.dp1, w.c1, w.part_1, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
@@ -1064,20 +918,19 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     if (paired) {
       // both gradients ran in the multi-job launch above
     } else if (h->band) {
-      const BandArgs ba{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B};
-      CHECK(launch_bandx<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0},
-                                          true));
+      const BandArgs ba{w.dp1, w.c1, nullptr, w.dp0, nullptr, nullptr, B};
+      CHECK(launch_band6<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0},
+                                           true));
     } else {
       ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
       CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV1_DGRAD, d, 1)));
     }
   }
   // conv0 (no input gradient: the frames are not trainable)
-  if (h->band && CH == 4 && h->split) {
+  if (h->band && CH == 4) {
     // slab count: one per CU where conv1's weight gradient can share the launch (on every launch
     // path, so they all sum the same slabs), else up to WG_P0S
-    const int P = (NS == 2 && conv1_pair_geometry(B, h->cus)) ? h->cus
-                                                              : std::min(WG_P0S, B * Conv0W<NS>::NBANDS);
+    const int P = conv1_pair_geometry(B, h->cus) ? h->cus : std::min(WG_P0S, B * Conv0W<2>::NBANDS);
     const Conv0WArgs a0{state, w.dp0, w.c0, w.part0, B, w.am(AM_DP0, h)};
     if (defer_w1) {
       // conv1's whole-channel weight gradient (MFMA-bound) beside conv0's (VALU-bound): one
@@ -1091,20 +944,17 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       CHECK(reduce_wgrad6<typename LY::W1>(h, s, wa, h->cus, grads + h->tensors[h->idx_conv[1]].offset));
     } else {
       ProbeScope ps(h, s, BA3C_K_CONV0_WGRAD);
-      HIP_TRY(launch_conv0s_wgrad(NS, dim3(P), s, a0));
+      HIP_TRY(launch_conv0s_wgrad(dim3(P), s, a0));
     }
     HIP_TRY(hipGetLastError());
     ReduceMap mp{};
     mp.kind = 0;
-    mp.M = Conv0W<NS>::M;
+    mp.M = Conv0W<2>::M;
     mp.N = 32;
     mp.cin = 4;
     mp.cinpad = 16;
     mp.dst = grads + h->tensors[h->idx_conv[0]].offset;
     CHECK(launch_reduce(h, s, w.part0, P, mp));
-  } else if (h->band && CH == 4) {
-    CHECK(launch_wgband<GWg0>(h, s, BA3C_K_CONV0_WGRAD, WgArgs{state, w.dp0, w.c0, w.part0, B}, WG_P0,
-                              grads + h->tensors[h->idx_conv[0]].offset, 16));
   } else {
     WgradPlan pl = plan_wgrad(25 * CH, 32, B * 6400, 128, 32);
     ConvWgrad<true, 84, 84, CH, 5, 5, 32, true> g{state, w.dp0, w.c0, w.part0, 1.0f / 255.0f, pl.M, pl.N, pl.K, pl.kchunk};
@@ -1169,6 +1019,7 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
     h->scalars_args = ScalarsJob::Args{w.terms, B, beta, w.relu, scalars};
     h->pend_scalars = true;      // launched by run_backward (conv3's weight gradient or finish)
   } else if (train && scalars && !fuse_scalars) {
+    ProbeScope ps(h, s, BA3C_K_SCALARS);
     hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, w.terms, B, beta, w.relu, scalars);
     HIP_TRY(hipGetLastError());
   }
@@ -1198,33 +1049,43 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   const int splits = c.replace_with_conv ? c.fc_splits : c.ps;
   if (splits < 1 || c.fc_neurons < 4 || c.fc_neurons % splits != 0 || (c.fc_neurons / splits) % 4 != 0)
     return fail(BA3C_ERR_INVALID, "fc_neurons must be a multiple of 4*fc_splits (or 4*ps)");
+  // launch-structure switches (each exercised by a GPU test; values outside the listed ones
+  // are rejected rather than coerced, so an A/B run measures what it asked for)
+  struct Switch {
+    const char* name;
+    int lo, hi;
+  };
+  static const Switch kSwitches[] = {{"BA3C_GENERIC", 0, 1},  {"BA3C_C1PAIR", 0, 2},   {"BA3C_SCALARS_RIDE", 0, 1},
+                                     {"BA3C_OVERLAP", 0, 2},  {"BA3C_MULTI", 0, 1},    {"BA3C_MULTI_BIG", 0, 3},
+                                     {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}};
+  int sw[8];
+  const int defaults[8] = {0, 2, 0, 2, 1, 3, 1, 1};
+  for (int i = 0; i < 8; ++i) {
+    sw[i] = defaults[i];
+    const char* e = getenv(kSwitches[i].name);
+    if (!e) continue;
+    if (!(e[0] >= '0' && e[0] <= '9' && e[1] == 0) || e[0] - '0' < kSwitches[i].lo || e[0] - '0' > kSwitches[i].hi)
+      return fail(BA3C_ERR_INVALID, std::string(kSwitches[i].name) + "=" + e + ": expected one digit in [" +
+                                        std::to_string(kSwitches[i].lo) + ", " + std::to_string(kSwitches[i].hi) + "]");
+    sw[i] = e[0] - '0';
+  }
   ba3c_handle* h = new ba3c_handle();
   h->cfg = c;
-  if (const char* e = getenv("BA3C_GENERIC")) h->band = !(e[0] == '1');
-  if (const char* e = getenv("BA3C_CONV0_F32")) h->split = !(e[0] == '1');
-  if (const char* e = getenv("BA3C_BAND6")) h->b6 = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_WGRAD6")) h->w6 = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_W6W")) h->w6w = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_C1PAIR")) h->c1pair = e[0] - '0';
-  if (const char* e = getenv("BA3C_SCALARS_RIDE")) h->scalars_ride = e[0] != '0';
-  if (const char* e = getenv("BA3C_OVERLAP")) h->overlap = e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2;
-  if (const char* e = getenv("BA3C_MULTI")) h->multi = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_MULTI_BIG")) h->multi_big = atoi(e) & 3;
-  if (const char* e = getenv("BA3C_FUSED_UPDATE")) h->fused_update = !(e[0] == '0');
-  if (const char* e = getenv("BA3C_PIPE")) h->pipe = (e[0] == '1');
-  if (const char* e = getenv("BA3C_RING")) h->ring = !(e[0] == '0');
+  h->band = sw[0] == 0;
+  h->c1pair = sw[1];
+  h->scalars_ride = sw[2] != 0;
+  h->overlap = sw[3];
+  h->multi = sw[4] != 0;
+  h->multi_big = sw[5];
+  h->fused_update = sw[6] != 0;
+  h->ring = sw[7] != 0;
+  h->g6 = h->band;
   {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
       h->cus = n;
   }
-  if (const char* e = getenv("BA3C_C0LAY")) h->c0lay = atoi(e) == 2 ? 2 : 3;
-  if (const char* e = getenv("BA3C_GEMM6")) h->g6 = !(e[0] == '0');
-  if (!h->band) h->g6 = false;
-  if (const char* e = getenv("BA3C_SPLIT")) h->ns = (std::strcmp(e, "bf16") == 0) ? 3 : 2;
-
-  if (!(h->band && h->b6 && h->w6 && h->split)) h->ns = 3;
 
   const int F = c.fc_neurons, per = F / splits;
   h->per = per;
@@ -1365,10 +1226,8 @@ int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
   Workspace w = carve(h, workspace, batch, false);
-  int r = h->cfg.channels == 4 ? (h->ns == 2 ? run_forward<4, 2>(h, s, params, state, batch, w, false)
-                                               : run_forward<4, 3>(h, s, params, state, batch, w, false))
-                               : (h->ns == 2 ? run_forward<12, 2>(h, s, params, state, batch, w, false)
-                                             : run_forward<12, 3>(h, s, params, state, batch, w, false));
+  int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, false)
+                               : run_forward<12>(h, s, params, state, batch, w, false);
   if (r != BA3C_OK) return r;
   return run_heads(h, s, params, w, batch, nullptr, nullptr, 0.f, explore_factor, false, probs,
                    probsT, value);
@@ -1411,26 +1270,20 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
   // no memset of `grads`: the backward pass's single reduction launch writes every element
   // of every tensor (incl. conv0's zero-padded channels)
   if (phase == 2)   // conv layers' backward on the workspace phase 1 left
-    return h->cfg.channels == 4 ? (h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads, 2)
-                                              : run_backward<4, 3>(h, s, params, state, batch, w, grads, 2))
-                                : (h->ns == 2 ? run_backward<12, 2>(h, s, params, state, batch, w, grads, 2)
-                                              : run_backward<12, 3>(h, s, params, state, batch, w, grads, 2));
-  // on the band + split path the weight-prep launch zeroes the ReLU counters
-  if (!(h->band && h->b6)) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_WORDS * 8, s));
-  int r = h->cfg.channels == 4 ? (h->ns == 2 ? run_forward<4, 2>(h, s, params, state, batch, w, true)
-                                               : run_forward<4, 3>(h, s, params, state, batch, w, true))
-                               : (h->ns == 2 ? run_forward<12, 2>(h, s, params, state, batch, w, true)
-                                             : run_forward<12, 3>(h, s, params, state, batch, w, true));
+    return h->cfg.channels == 4 ? run_backward<4>(h, s, params, state, batch, w, grads, 2)
+                                : run_backward<12>(h, s, params, state, batch, w, grads, 2);
+  // on the split path the weight-prep launch zeroes the ReLU counters
+  if (!h->band) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_WORDS * 8, s));
+  int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, true)
+                               : run_forward<12>(h, s, params, state, batch, w, true);
   if (r != BA3C_OK) return r;
   // heads + loss + its gradient, fc1's split-K finish and (last workgroup) the TfDictOp scalars
   h->pend_scalars = false;
   CHECK(run_heads(h, s, params, w, batch, action, futurereward, entropy_beta, 1.0f, true, nullptr,
                   nullptr, nullptr, scalars, phase == 0 && h->scalars_ride && h->g6));
   if (h->cfg.channels == 4)
-    return h->ns == 2 ? run_backward<4, 2>(h, s, params, state, batch, w, grads, phase)
-                      : run_backward<4, 3>(h, s, params, state, batch, w, grads, phase);
-  return h->ns == 2 ? run_backward<12, 2>(h, s, params, state, batch, w, grads, phase)
-                    : run_backward<12, 3>(h, s, params, state, batch, w, grads, phase);
+    return run_backward<4>(h, s, params, state, batch, w, grads, phase);
+  return run_backward<12>(h, s, params, state, batch, w, grads, phase);
 }
 
 int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* workspace, int32_t t0,
@@ -1649,13 +1502,13 @@ int ba3c_kernel_split(const ba3c_handle* h, int32_t kid) {
   const bool c4 = h->cfg.channels == 4;
   switch (kid) {
     case BA3C_K_CONV0_FWD:
-    case BA3C_K_CONV0_WGRAD: return (h->band && c4 && h->split) ? h->ns : (h->g6 ? 6 : 1);
+    case BA3C_K_CONV0_WGRAD: return (h->band && c4) ? 2 : (h->g6 ? 6 : 1);
     case BA3C_K_CONV1_FWD:
     case BA3C_K_CONV2_FWD:
     case BA3C_K_CONV1_DGRAD:
-    case BA3C_K_CONV2_DGRAD: return (h->band && h->b6) ? (h->ns == 2 ? 3 : 6) : 1;
+    case BA3C_K_CONV2_DGRAD:
     case BA3C_K_CONV1_WGRAD:
-    case BA3C_K_CONV2_WGRAD: return (h->band && h->w6) ? (h->ns == 2 ? 3 : 6) : 1;
+    case BA3C_K_CONV2_WGRAD: return h->band ? 3 : 1;
     case BA3C_K_CONV3_FWD:
     case BA3C_K_CONV3_DGRAD:
     case BA3C_K_CONV3_WGRAD:
@@ -1684,8 +1537,8 @@ int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {
                           kid == BA3C_K_CONV2_FWD || kid == BA3C_K_CONV1_DGRAD || kid == BA3C_K_CONV2_DGRAD ||
                           kid == BA3C_K_CONV1_WGRAD || kid == BA3C_K_CONV2_WGRAD;
   if (kid == BA3C_K_CONV0_FWD || kid == BA3C_K_CONV0_WGRAD)
-    if (!(h->band && h->cfg.channels == 4 && h->split)) return 3;
-  return band_split && h->ns == 2 ? 2 : 3;
+    if (!(h->band && h->cfg.channels == 4)) return 3;
+  return band_split ? 2 : 3;
 }
 
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {

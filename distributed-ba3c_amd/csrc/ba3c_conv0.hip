@@ -13,11 +13,8 @@
 
 namespace ba3c {
 
-hipError_t launch_conv0s_fwd(int ns, int lay, dim3 grid, hipStream_t s, const Conv0SArgs& a) {
-  if (ns == 2 && lay == 3) hipLaunchKernelGGL((conv0s_fwd_kernel<2, 3>), grid, dim3(256), 0, s, a);
-  else if (ns == 2) hipLaunchKernelGGL((conv0s_fwd_kernel<2, 2>), grid, dim3(256), 0, s, a);
-  else if (lay == 3) hipLaunchKernelGGL((conv0s_fwd_kernel<3, 3>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((conv0s_fwd_kernel<3, 2>), grid, dim3(256), 0, s, a);
+hipError_t launch_conv0s_fwd(dim3 grid, hipStream_t s, const Conv0SArgs& a) {
+  hipLaunchKernelGGL(conv0s_fwd_kernel, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -47,9 +44,8 @@ hipError_t launch_wgrad01_pair(hipStream_t s, const Wg6Args& a1, int g1, const C
   return hipGetLastError();
 }
 
-hipError_t launch_conv0s_wgrad(int ns, dim3 grid, hipStream_t s, const Conv0WArgs& a) {
-  if (ns == 2) hipLaunchKernelGGL(conv0s_wgrad_kernel<2>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(conv0s_wgrad_kernel<3>, grid, dim3(256), 0, s, a);
+hipError_t launch_conv0s_wgrad(dim3 grid, hipStream_t s, const Conv0WArgs& a) {
+  hipLaunchKernelGGL(conv0s_wgrad_kernel<2>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

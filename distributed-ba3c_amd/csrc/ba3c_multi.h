@@ -71,21 +71,19 @@ struct Gemm6Job {
   }
 };
 
-template <int NS, int LAY>
 struct Conv0SJob {
   using Args = Conv0SArgs;
-  static constexpr int LDS = conv0s_fwd_lds_bytes<LAY>();
+  static constexpr int LDS = conv0s_fwd_lds_bytes();
   __device__ static void run(const Args& a, int x, int, int, int gx, char* lds, uint32_t*) {
-    conv0s_fwd_body<NS, LAY>(a, x, gx, lds);
+    conv0s_fwd_body(a, x, gx, lds);
   }
 };
 
-template <int NS>
 struct WPrep6Job {
   using Args = WPrep6Args;
   static constexpr int LDS = 0;
   __device__ static void run(const Args& a, int x, int y, int, int gx, char*, uint32_t* red4) {
-    wprep6_body<NS>(a, x, y, gx, reinterpret_cast<float*>(red4));
+    wprep6_body(a, x, y, gx, reinterpret_cast<float*>(red4));
   }
 };
 

@@ -83,7 +83,7 @@ __device__ __forceinline__ UnpoolRaw unpool4(const float* __restrict__ dP, const
 
 // ------------------------------------------------------------------------------------
 // Forward conv (Conv2D VALID stride 1, no bias; models/conv2d.py:63-73, train.py:177-212)
-// MODE 0: ReLU + 2x2 max-pool + argmax code (training)   MODE 1: same without codes
+// MODE 0: ReLU + 2x2 max-pool + argmax code (codes when `code` is set)   MODE 1: same without codes
 // MODE 2: ReLU only, plain NHWC store (conv3)
 // M rows: MODE 0/1 = (n, ph, pw, sub) so a lane's 4 consecutive accumulator rows are one
 // pooling window; MODE 2 = (n, oh, ow).  K = (kh, kw, c) over the REAL input channels
@@ -175,7 +175,7 @@ struct ConvFwd {
               out[(size_t)win * COUT + col] = o;
               if (win / WPI == n0) m0 = fmaxf(m0, o);
               else m1 = fmaxf(m1, o);
-              if constexpr (MODE == 0) code[(size_t)win * COUT + col] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
+              if (MODE == 0 && code) code[(size_t)win * COUT + col] = mx > 0.f ? (uint8_t)arg : (uint8_t)255;
             }
           }
         } else {

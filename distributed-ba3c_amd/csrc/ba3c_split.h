@@ -141,9 +141,6 @@ struct Conv0S {
   static constexpr int HS = 84, WS = 84, C = 4, COUT = 32, KT = 5, NTAP = 25;
   static constexpr int HO = 80, WO = 80, RB = 16, NBANDS = HO / RB, SROWS = RB + KT - 1;
   static constexpr int KSTEPS = 4;                 // 4 x 32 K = 32 tap slots (25 used)
-  // LDS row pitch (pixels) of layout LAY: 0 = dense 84 with taps in order (r01), 1 = 88 with
-  // taps in order, 2 / 3 = 88 with the paired tap orders (conv0_atap); 704 B = 64 mod 256
-  __host__ __device__ static constexpr int xp(int lay) { return lay ? 88 : 84; }
   static constexpr int MAXSPLIT = 3;
   static constexpr int PROWS_W = RB / 2 / 4;       // pooled rows per wave (2)
   static constexpr int MBROW = (WO / 2) / 4;       // m-blocks per pooled row (10)
@@ -154,43 +151,23 @@ struct Conv0S {
   static_assert(RB % 8 == 0 && HO % RB == 0 && MBW % MCH == 0, "conv0 split geometry");
 };
 
-// K order of conv0's forward: slot (kstep s, lane group q, tap half h) -> tap.  Slot pair
-// p = 4s + 2(q >> 1) + h holds taps (p, p + 10) in lane groups q = 2(q >> 1) and + 1, i.e.
-// (kh, kw) and (kh + 2, kw): with the 88-pixel LDS row pitch (704 B = 64 mod 256) the four
-// 64-byte pixel runs a 32-lane half reads (2 rows x 2 lane groups) land in four distinct
-// bank windows, and a 16-lane group's two rows in two (ds_read_b64 / ds_read2_b64 both
-// conflict-free; r01 v7 measured 48 % conflict cycles on the 84-pixel, tap-order layout).
-// Pairs p = 10..14 carry only tap p + 10 (kh = 4): their even slot is padding (weight 0)
-// that reads tap p's address; pair 15 is padding in both slots (addresses of taps 0, 10).
-__host__ __device__ constexpr int conv0_pair(int s, int q, int h) { return 4 * s + 2 * (q >> 1) + h; }
-// the tap whose pixels slot (s, q, h) reads (always a real tap: in-bounds, finite values);
-// layouts 0 / 1 keep the plain order tap = 8s + 2q + h (padding slots read tap 0)
-//
-// Layout 3 (default): the two taps of a LANE's A fragment are (t, t + 10) = (kh, kw) and
-// (kh + 2, kw), two LDS rows apart for every lane and k-step, so the fragment is ONE
-// ds_read2_b64 into four consecutive VGPRs (r02's layout 2 needed two reads whose registers
-// the compiler then copied together: ~3 v_mov per fragment).  Pair P = 4s + q: P < 10 holds
-// taps (P, P + 10); P = 10..14 holds (P, P + 10) with the first half padding (weight 0, reads
-// the in-band row kh = 2) and the second the kh = 4 tap; P = 15 is padding in both halves.
-// A 16-lane group reads 2 rows x 8 pixels of 8 B; with the 88-pixel pitch (704 B = 64 mod 128)
-// those 16 addresses are distinct mod 128 B: conflict-free for ds_read2_b64's 4 x 16 groups.
-__host__ __device__ constexpr int conv0_atap(int s, int q, int h, int lay = 2) {
-  return lay == 3 ? (4 * s + q < 15 ? 4 * s + q : 0) + 10 * h
-       : lay == 2 ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) : 0) + 10 * (q & 1)
-                  : (8 * s + 2 * q + h < 25 ? 8 * s + 2 * q + h : 0);
-}
+// K order of conv0's forward: the two taps of a LANE's A fragment are (t, t + 10) = (kh, kw)
+// and (kh + 2, kw), two LDS rows apart for every lane and k-step, so the fragment is ONE
+// 16-byte LDS entry (see C0E_ROWS).  Pair P = 4s + q: P < 10 holds taps (P, P + 10);
+// P = 10..14 holds (P, P + 10) with the first half padding (weight 0, reads the in-band row
+// kh = 2) and the second the kh = 4 tap; P = 15 is padding in both halves.  A 16-lane group
+// reads 2 rows x 8 pixels; with the 88-entry pitch those 16 addresses are distinct mod 128 B.
+// The tap whose pixels slot (s, q, h) reads (always a real tap: in-bounds, finite values):
+__host__ __device__ constexpr int conv0_atap(int s, int q, int h) { return (4 * s + q < 15 ? 4 * s + q : 0) + 10 * h; }
 // the tap whose weight slot (s, q, h) carries, -1 for padding
-__host__ __device__ constexpr int conv0_wtap(int s, int q, int h, int lay = 2) {
-  return lay == 3 ? (4 * s + q < 10 ? 4 * s + q + 10 * h : (4 * s + q < 15 && h ? 4 * s + q + 10 : -1))
-       : lay == 2 ? ((q & 1) ? (conv0_pair(s, q, h) < 15 ? conv0_pair(s, q, h) + 10 : -1)
-                             : (conv0_pair(s, q, h) < 10 ? conv0_pair(s, q, h) : -1))
-                  : (8 * s + 2 * q + h < 25 ? 8 * s + 2 * q + h : -1);
+__host__ __device__ constexpr int conv0_wtap(int s, int q, int h) {
+  return 4 * s + q < 10 ? 4 * s + q + 10 * h : (4 * s + q < 15 && h ? 4 * s + q + 10 : -1);
 }
 
 // real-channel weight of conv0/W [5,5,16,32] (TARGET_CHANNELS = 16, train.py:99) at
 // K position (kstep s, lane group q, element e) = tap conv0_wtap(s, q, e >> 2), channel e & 3
-__device__ __forceinline__ float conv0_w(const float* __restrict__ w, int s, int q, int e, int n, int lay) {
-  const int tap = conv0_wtap(s, q, e >> 2, lay), c = e & 3;
+__device__ __forceinline__ float conv0_w(const float* __restrict__ w, int s, int q, int e, int n) {
+  const int tap = conv0_wtap(s, q, e >> 2), c = e & 3;
   return tap >= 0 ? w[((size_t)tap * 16 + c) * 32 + n] : 0.f;
 }
 
@@ -208,36 +185,24 @@ __device__ __forceinline__ float conv0_wmax_block(const float* __restrict__ w, f
   return fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
 }
 
-// conv0 weights -> NS split planes in MFMA B-fragment order (NS = 2: scaled by 2^kexp).
-// One thread per (nt, kstep, lane).
-template <int NS>
+// conv0 weights -> 2 fp16 split planes of w * 2^kexp in MFMA B-fragment order.  One thread
+// per (nt, kstep, lane).
 __device__ __forceinline__ void conv0s_wprep_one(const float* __restrict__ w, uint4* __restrict__ wb, int t,
-                                                 int kexp, int lay = 2) {
+                                                 int kexp) {
   using G = Conv0S;
   if (t >= 2 * G::KSTEPS * 64) return;
   const int lane = t & 63, s = (t >> 6) % G::KSTEPS, nt = t / (64 * G::KSTEPS);
   const int n = nt * 16 + (lane & 15), q = lane >> 4;
   const float sc = exp2i(kexp);
-  uint32_t part[NS][8];
+  uint32_t part[2][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float v = conv0_w(w, s, q, e, n, lay);
-    if constexpr (NS == 3) split3(v, part[0][e], part[1][e], part[2][e]);
-    else split2(v * sc, part[0][e], part[1][e]);
-  }
+  for (int e = 0; e < 8; ++e) split2(conv0_w(w, s, q, e, n) * sc, part[0][e], part[1][e]);
 #pragma unroll
-  for (int sp = 0; sp < NS; ++sp)
+  for (int sp = 0; sp < 2; ++sp)
     wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane] =
         make_uint4(part[sp][0] | (part[sp][1] << 16), part[sp][2] | (part[sp][3] << 16),
                    part[sp][4] | (part[sp][5] << 16), part[sp][6] | (part[sp][7] << 16));
 }
-
-#if BA3C_SHARED_KERNELS  // non-template kernel: emitted by ba3c_capi.hip only
-__global__ void __launch_bounds__(256) conv0s_wprep_kernel(const float* __restrict__ w,
-                                                           uint4* __restrict__ wb, int lay) {
-  conv0s_wprep_one<3>(w, wb, blockIdx.x * 256 + threadIdx.x, 0, lay);
-}
-#endif
 
 // Persistent workgroups walk bands (one image x RB output rows = RB/2 pooled rows); wave w
 // owns pooled rows 2w, 2w+1 of a band = 20 m-blocks of 4 windows, both 16-channel n-tiles.
@@ -289,15 +254,11 @@ __device__ __forceinline__ void u8quad(uint32_t px, uint32_t& o01, uint32_t& o23
   }
 }
 
-template <int LAY>
-constexpr int conv0s_band_bytes() {
-  return LAY == 3 ? C0E_ROWS * C0E_PITCH * 16 : Conv0S::SROWS * Conv0S::xp(LAY) * 8;
-}
+constexpr int conv0s_band_bytes() { return C0E_ROWS * C0E_PITCH * 16; }
 // per wave: one pooled row of the band's output (40 windows x 32 channels) as fp32 + codes,
 // staged so the global stores are whole 16-byte pieces (see the epilogue)
 constexpr int C0_WST_BYTES = (Conv0S::WO / 2) * Conv0S::COUT * 5;
-template <int LAY>
-constexpr int conv0s_fwd_lds_bytes() { return conv0s_band_bytes<LAY>() + 4 * C0_WST_BYTES; }
+constexpr int conv0s_fwd_lds_bytes() { return conv0s_band_bytes() + 4 * C0_WST_BYTES; }
 
 // raw buffer resource over `base` (gfx9 descriptor word 3; offsets stay < 2^31 bytes)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
@@ -311,81 +272,50 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
 __device__ __forceinline__ int pos01(int bits) { return bits > 0 ? 1 : 0; }
 
 // bx / gx: first band and persistent stride (blockIdx.x / gridDim.x of a plain launch);
-// lds: conv0s_fwd_lds_bytes<LAY>() bytes
-template <int NS, int LAY = 2, bool TRAIN = true>
+// lds: conv0s_fwd_lds_bytes() bytes
+template <bool TRAIN>
 __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, int gx, char* lds);
 
-template <int NS, int LAY = 2>
 __device__ __forceinline__ void conv0s_fwd_body(const Conv0SArgs& a, int bx, int gx, char* lds) {
   // training (codes + ReLU count) and predictor variants: no per-store branch in the loop
-  if (a.out_code) conv0s_fwd_body_t<NS, LAY, true>(a, bx, gx, lds);
-  else conv0s_fwd_body_t<NS, LAY, false>(a, bx, gx, lds);
+  if (a.out_code) conv0s_fwd_body_t<true>(a, bx, gx, lds);
+  else conv0s_fwd_body_t<false>(a, bx, gx, lds);
 }
 
-template <int NS, int LAY, bool TRAIN>
+template <bool TRAIN>
 __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, int gx, char* lds) {
   using G = Conv0S;
-  constexpr int XP = G::xp(LAY);
-  using SP = SplitP<NS>;
-  uint2* xs = reinterpret_cast<uint2*>(lds);        // 16-bit pixels (4 channels), 14 KB
+  using SP = SplitP<2>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbands = a.batch * G::NBANDS;
 
-  // ---- rows [y0, y0 + SROWS) of a band ----
-  // layouts 0-2: contiguous 16-byte loads (4 pixels), converted and stored as one run.
-  // Layout 3: one thread per 16-byte ENTRY (r, x) = [pixel (r, x) | pixel (r + 2, x)]: two dword
-  // loads (coalesced over consecutive x), one ds_write_b128 — consecutive lanes write
-  // consecutive entries, conflict-free (r03e PMC: the 4-pixel runs written as 8-byte halves at a
-  // 64-byte lane stride made 52 % of the LDS cycles bank conflicts)
-  constexpr int NV = LAY == 3 ? C0E_ROWS * G::WS : G::SROWS * G::WS / 4;   // entries / uint4
+  // ---- rows [y0, y0 + SROWS) of a band: one thread per 16-byte ENTRY (r, x) = [pixel (r, x)
+  // | pixel (r + 2, x)]: two dword loads (coalesced over consecutive x), one ds_write_b128 —
+  // consecutive lanes write consecutive entries, conflict-free (r03e PMC: the 4-pixel runs
+  // written as 8-byte halves at a 64-byte lane stride made 52 % of the LDS cycles conflicts)
+  constexpr int NV = C0E_ROWS * G::WS;             // entries
   constexpr int NPT = (NV + 255) / 256;
-  uint4 v[LAY == 3 ? 1 : NPT];
-  uint32_t ev[LAY == 3 ? NPT : 1][2];
+  uint32_t ev[NPT][2];
   auto load_band = [&](int band) {
     const int img = band / G::NBANDS, y0 = (band - img * G::NBANDS) * G::RB;
-    if constexpr (LAY == 3) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
 #pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const int e = tid + 256 * i;               // entry e = row r * 84 + x: pixel index e
-        ev[i][0] = e < NV ? src[e] : 0u;
-        ev[i][1] = e < NV ? src[e + 2 * G::WS] : 0u;
-      }
-    } else {
-      const uint4* src = reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C);
-#pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const int f = tid + 256 * i;
-        v[i] = f < NV ? src[f] : make_uint4(0, 0, 0, 0);
-      }
+    for (int i = 0; i < NPT; ++i) {
+      const int e = tid + 256 * i;                 // entry e = row r * 84 + x: pixel index e
+      ev[i][0] = e < NV ? src[e] : 0u;
+      ev[i][1] = e < NV ? src[e + 2 * G::WS] : 0u;
     }
   };
   auto store_band = [&]() {
-    if constexpr (LAY == 3) {
 #pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const int e = tid + 256 * i;
-        if (e < NV) {
-          const int r = e / G::WS, x = e - r * G::WS;
-          uint32_t o[4];
+    for (int i = 0; i < NPT; ++i) {
+      const int e = tid + 256 * i;
+      if (e < NV) {
+        const int r = e / G::WS, x = e - r * G::WS;
+        uint32_t o[4];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) u8quad<NS>(ev[i][h], o[2 * h], o[2 * h + 1]);
-          reinterpret_cast<uint4*>(lds)[r * C0E_PITCH + x] = make_uint4(o[0], o[1], o[2], o[3]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NPT; ++i) {
-        const int f = tid + 256 * i;
-        if (f < NV) {
-          const uint32_t px[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-          uint32_t o[8];
-#pragma unroll
-          for (int p = 0; p < 4; ++p) u8quad<NS>(px[p], o[2 * p], o[2 * p + 1]);
-          const int px0 = 4 * f, r = px0 / G::WS, lp = r * XP + (px0 - r * G::WS);   // 4 px of one row
-          reinterpret_cast<uint4*>(xs + lp)[0] = make_uint4(o[0], o[1], o[2], o[3]);
-          reinterpret_cast<uint4*>(xs + lp)[1] = make_uint4(o[4], o[5], o[6], o[7]);
-        }
+        for (int h = 0; h < 2; ++h) u8quad<2>(ev[i][h], o[2 * h], o[2 * h + 1]);
+        reinterpret_cast<uint4*>(lds)[r * C0E_PITCH + x] = make_uint4(o[0], o[1], o[2], o[3]);
       }
     }
   };
@@ -394,9 +324,9 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
   if (band < nbands) load_band(band);
 
   const int li = lane & 15, lq = lane >> 4;
-  u32x4 wf[NS][2][G::KSTEPS];
+  u32x4 wf[2][2][G::KSTEPS];
 #pragma unroll
-  for (int sp = 0; sp < NS; ++sp)
+  for (int sp = 0; sp < 2; ++sp)
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -406,28 +336,27 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
       }
   // this lane's row (window li>>2, sub li&3) of m-block 0 of the wave, per (kstep, tap half)
   const int wi = li >> 2, sub = li & 3;
-  // (layout 3: entry index, pitch C0E_PITCH; else pixel index, pitch XP)
-  constexpr int RP = LAY == 3 ? C0E_PITCH : XP;
+  constexpr int RP = C0E_PITCH;                     // entry index pitch
   const int pix0 = (4 * wave + (sub >> 1)) * RP + 2 * wi + (sub & 1);
   int lb[G::KSTEPS][2];
 #pragma unroll
   for (int s = 0; s < G::KSTEPS; ++s)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int tap = conv0_atap(s, lq, h, LAY);
+      const int tap = conv0_atap(s, lq, h);
       lb[s][h] = pix0 + (tap / G::KT) * RP + tap % G::KT;
     }
 
   int pos = 0;                                      // this lane's ReLU positives (TRAIN)
   // (sum_k u8 * w 2^kw) * (2^-kw / 255): scaling by a power of two commutes with the rounding
-  const float oscale = NS == 2 ? (1.0f / 255.0f) * exp2i(-a.wexp[0]) : 1.0f / 255.0f;
+  const float oscale = (1.0f / 255.0f) * exp2i(-a.wexp[0]);
   // Epilogue stores go through a wave-private LDS area holding one pooled row of outputs
   // (40 windows x 32 channels: 5 KB fp32 + 1.25 KB codes, contiguous in global memory too):
   // each lane writes its window / channel values there, then the wave copies the row out in
   // 16-byte pieces, consecutive lanes consecutive pieces — 7 buffer_store_dwordx4 per pooled
   // row instead of 40 dword + 40 byte stores (r03i: a byte store per value cost ~7 cycles of
   // the CU's store path each)
-  float* wst = reinterpret_cast<float*>(lds + conv0s_band_bytes<LAY>() + wave * C0_WST_BYTES);
+  float* wst = reinterpret_cast<float*>(lds + conv0s_band_bytes() + wave * C0_WST_BYTES);
   uint8_t* wsc = reinterpret_cast<uint8_t*>(wst + (G::WO / 2) * G::COUT);
   const int lane_el = lq * G::COUT + li;           // (window lq, channel li) in the row area
   for (; band < nbands; band += gx) {
@@ -455,17 +384,12 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
         for (int j = 0; j < G::MCH; ++j) {
           const int jj = ch * G::MCH + j;
           const int off = (jj / G::MBROW) * 2 * RP + (jj % G::MBROW) * 8;   // immediate
-          if constexpr (LAY == 3) {
-            // both taps of the fragment in one 16-byte entry: one ds_read_b128
-            const uint4 u = reinterpret_cast<const uint4*>(lds)[lb[s][0] + off];
-            af[j] = u32x4{u.x, u.y, u.z, u.w};
-          } else {
-            const uint2 p0 = xs[lb[s][0] + off], p1 = xs[lb[s][1] + off];
-            af[j] = u32x4{p0.x, p0.y, p1.x, p1.y};
-          }
+          // both taps of the fragment in one 16-byte entry: one ds_read_b128
+          const uint4 u = reinterpret_cast<const uint4*>(lds)[lb[s][0] + off];
+          af[j] = u32x4{u.x, u.y, u.z, u.w};
         }
 #pragma unroll
-        for (int sp = 0; sp < NS; ++sp)
+        for (int sp = 0; sp < 2; ++sp)
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -526,16 +450,17 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
       }
     }
     // max over the window maxima, then the scale: a positive scale is monotone in fp32
-    if constexpr (NS == 2) amax_publish(a.amax_out, img, __int_as_float(bmaxi) * oscale, lane);
+    amax_publish(a.amax_out, img, __int_as_float(bmaxi) * oscale, lane);
   }
   if (TRAIN && a.relu_count) relu_count_add(a.relu_count, (unsigned long long)pos, lane);
 }
 
-template <int NS, int LAY = 2>
+#if !BA3C_SHARED_KERNELS  // emitted by ba3c_conv0.hip only
 __global__ void __launch_bounds__(256) conv0s_fwd_kernel(const Conv0SArgs a) {
-  __shared__ uint4 xs4[conv0s_fwd_lds_bytes<LAY>() / 16];
-  conv0s_fwd_body<NS, LAY>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(xs4));
+  __shared__ uint4 xs4[conv0s_fwd_lds_bytes() / 16];
+  conv0s_fwd_body(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(xs4));
 }
+#endif
 
 // ---------------------------------------------------------------------------------------
 // conv0 weight gradient (Conv2DBackpropFilter of conv0, train.py:177 under TF autodiff):

@@ -261,6 +261,9 @@ def test_large_batch_launch_structures_match_default(monkeypatch, var, base, mod
         dp0 = eng.workspace_tensor("dp0", B).clone()
         torch.cuda.synchronize()
         out.append((eng.grads.clone(), sc.clone(), dp0))
+        if var == "BA3C_SCALARS_RIDE":
+            # the reduction really ran inside conv3's weight-gradient launch (or on its own)
+            assert ("scalars" in eng.kernel_merged("conv3_wgrad")) == (env == "1")
         del eng
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])

@@ -1,0 +1,91 @@
+"""Every launch-structure switch ba3c_create reads (BA3C_GENERIC, _C1PAIR, _SCALARS_RIDE,
+_OVERLAP, _MULTI, _MULTI_BIG, _FUSED_UPDATE, _RING) held to the oracle: one training pass at
+configs[1]'s B=32 (F=128, S=4) and at B=160 (F=512, S=1: the bench geometry above SMALL_B) —
+every gradient within 1e-4 and the TfDictOp scalars against the fp64 oracle driven by the
+run's own discrete decisions (train.py:164-327, multigpu.py:85-86) — then one fused clip + Adam
+apply against the oracle's TF Adam on the clipped oracle gradients (train.py:329-330, 582-597).
+Out-of-range values are rejected by ba3c_create (no silent coercion)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ba3c_oracle as O
+from test_gpu_parity import GRAD_TOL, as64, case, dev, gpu_decisions, rel
+
+pytestmark = pytest.mark.gpu
+
+SETTINGS = [("BA3C_GENERIC", "1"), ("BA3C_C1PAIR", "0"), ("BA3C_C1PAIR", "1"),
+            ("BA3C_SCALARS_RIDE", "1"), ("BA3C_OVERLAP", "0"), ("BA3C_OVERLAP", "1"),
+            ("BA3C_MULTI", "0"), ("BA3C_MULTI_BIG", "0"), ("BA3C_FUSED_UPDATE", "0"),
+            ("BA3C_RING", "0"), (None, None)]
+GEOM = {32: dict(A=4, C=4, F=128, S=4), 160: dict(A=4, C=4, F=512, S=1)}
+_REF = {}
+
+
+def _reference(B, params, state, action, R, cfg, forced):
+    """Oracle pass for these decisions (cached: most settings make identical decisions)."""
+    for key, val in _REF.items():
+        if key[0] == B and all(np.array_equal(val[0][k], forced[k]) for k in forced):
+            return val[1]
+    ref = O.loss_and_grads_chunked(as64(params), state, action, R.astype(np.float64), cfg,
+                                   forced=forced, chunk=16)
+    _REF[(B, len(_REF))] = ({k: v.copy() for k, v in forced.items()}, ref)
+    return ref
+
+
+@pytest.mark.parametrize("B", [32, 160])
+@pytest.mark.parametrize("var,val", SETTINGS)
+def test_switch_matches_oracle(monkeypatch, B, var, val):
+    from ba3c_amd._lib import SCALAR_NAMES
+    from ba3c_amd.engine import Ba3cEngine
+    from ba3c_amd.optimizer import AdamOptimizer
+    for v, _ in SETTINGS:
+        if v:
+            monkeypatch.delenv(v, raising=False)
+    if var:
+        monkeypatch.setenv(var, val)
+    g_ = GEOM[B]
+    params, state, action, R, cfg = case(3200 + B, B, wscale=2.0, **g_)
+    eng = Ba3cEngine(num_actions=g_["A"], channels=g_["C"], fc_neurons=g_["F"], fc_splits=g_["S"],
+                     max_batch=B)
+    eng.load_params(params)
+    sc = eng.train_grads(dev(state), dev(action), dev(R), entropy_beta=0.01)
+    got = eng.state_dict(eng.grads)
+    forced, codes = gpu_decisions(eng, B)
+    t, osc, g = _reference(B, params, state, action, R, cfg, forced)
+    for layer in range(3):
+        assert np.mean(t["own_c%d" % layer] != codes[layer]) < 1e-4, layer
+    for k in g:
+        e = rel(got[k], g[k])
+        assert e < GRAD_TOL, (var, val, k, e)
+    s = sc.cpu().numpy()
+    for i, name in enumerate(SCALAR_NAMES[:7]):
+        ref = float(osc[name])
+        assert abs(s[i] - ref) <= 1e-4 * max(1.0, abs(ref)), (name, s[i], ref)
+    assert abs(int(s[7]) - osc["active_relus"]) <= max(2, 1e-5 * osc["active_relus"])
+    # one fused clip + Adam apply (README best hyper-parameters) on these gradients
+    opt = AdamOptimizer(1e-3, beta1=0.8, beta2=0.75, epsilon=1e-8)
+    opt.apply_gradients(eng, fuse_clip=True)
+    newp = eng.state_dict()
+    assert eng.device_errors() == 0
+    for k in g:
+        gc = O.clip_by_average_norm(g[k])
+        pk, _, _ = O.apply_adam(as64(params)[k], gc, np.zeros_like(gc), np.zeros_like(gc), 1e-3, 0.8,
+                                0.75, 1e-8, np.float32(0.8), np.float32(0.75))
+        d_got = newp[k].astype(np.float64) - params[k]
+        d_ref = pk - params[k]
+        mask = np.abs(g[k]) > 1e-4 * max(np.abs(g[k]).max(), 1e-30)
+        if mask.any():
+            assert rel(d_got[mask], d_ref[mask]) < GRAD_TOL, (var, val, k)
+    del eng
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("var,val", [("BA3C_C1PAIR", "3"), ("BA3C_RING", "yes"), ("BA3C_OVERLAP", ""),
+                                     ("BA3C_MULTI_BIG", "12")])
+def test_switch_rejects_out_of_range_values(monkeypatch, var, val):
+    from ba3c_amd import Ba3cLibraryError
+    from ba3c_amd.engine import Ba3cEngine
+    monkeypatch.setenv(var, val)
+    with pytest.raises(Ba3cLibraryError, match=var):
+        Ba3cEngine(num_actions=4, channels=4, fc_neurons=128, fc_splits=4, max_batch=8)
