@@ -264,12 +264,6 @@ constexpr int conv0s_fwd_lds_bytes() { return conv0s_band_bytes() + 4 * C0_WST_B
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
 }
-// ReLU positive test of an fp32 value by its bits as a signed integer: bits > 0 exactly for
-// x > 0 (+0 -> 0, negatives -> 0; -0 cannot come out of an accumulator that starts at +0).
-// Compiler-visible code only: an inline-asm v_med3_i32 here read MFMA results without the
-// wait states the hazard recognizer inserts for real VALU instructions (r03f: a stale ReLU
-// count), so the compiler's compare + carry-add form stays.
-__device__ __forceinline__ int pos01(int bits) { return bits > 0 ? 1 : 0; }
 
 // bx / gx: first band and persistent stride (blockIdx.x / gridDim.x of a plain launch);
 // lds: conv0s_fwd_lds_bytes() bytes
@@ -286,7 +280,8 @@ template <bool TRAIN>
 __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, int gx, char* lds) {
   using G = Conv0S;
   using SP = SplitP<2>;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index in an SGPR: the wave's LDS areas and output rows are scalar arithmetic
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nbands = a.batch * G::NBANDS;
 
   // ---- rows [y0, y0 + SROWS) of a band: one thread per 16-byte ENTRY (r, x) = [pixel (r, x)
@@ -418,7 +413,12 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
             arg = b1 == m ? 1u : arg;
             arg = b0 == m ? 0u : arg;
             wsc[lane_el + cofs] = (uint8_t)(m != 0 ? arg : 255u);
-            pos += pos01(b0) + pos01(b1) + pos01(b2) + pos01(b3);
+            // positives by v_cmp -> SGPR mask -> s_bcnt1 (one VALU instruction per value; the
+            // bits compare as signed integers: x > 0 exactly for positive x)
+            // ReLU positives: the bits compare as signed integers (x > 0 exactly for x > 0).
+            // Per-lane compare + add; a v_cmp -> SGPR ballot + s_bcnt1 form has fewer VALU
+            // instructions but measured slower (0.189 -> 0.209 ms, VALU-to-SALU dependencies)
+            pos += (b0 > 0) + (b1 > 0) + (b2 > 0) + (b3 > 0);
             // materialise the count here: otherwise it is sunk to its only use after the band
             // loop, keeping every accumulator of the chunk live (r03g: > 256 registers)
             asm volatile("" : "+v"(pos));
@@ -549,7 +549,7 @@ __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, i
   uint16_t* ys = reinterpret_cast<uint16_t*>(lds);
   uint16_t* xs = ys + G::Y_16;
   uint8_t* yc8 = reinterpret_cast<uint8_t*>(xs + G::X_16);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4;
   const int nbands = a.batch * G::NBANDS;
   const int ky = NS == 2 ? amax_exp(amax_all(a.amax_dp, a.batch, red4)) : 0;
