@@ -96,8 +96,9 @@ struct ba3c_handle {
   int c1pair = 2;
   uint32_t merged[BA3C_NUM_KERNELS] = {};   // ba3c_kernel_merged, per training pass
   // large-batch scalar reduction deferred from run_heads onto conv3's weight-gradient launch
-  // (one-pass backward only; BA3C_SCALARS_RIDE=1; default: its own launch after the heads)
-  bool scalars_ride = false;
+  // (one-pass backward only; default; BA3C_SCALARS_RIDE=0: its own launch after the heads).
+  // r04 same-box A/B: step 1.954 -> 1.935 ms, conv3's weight-gradient launch +1.6 us
+  bool scalars_ride = true;
   bool pend_scalars = false;
   ScalarsJob::Args scalars_args{};
   // conv1 fwd / dgrad (multi-band layouts) as ring-walk persistent kernels at batches that
@@ -1059,7 +1060,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
                                      {"BA3C_OVERLAP", 0, 2},  {"BA3C_MULTI", 0, 1},    {"BA3C_MULTI_BIG", 0, 3},
                                      {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}};
   int sw[8];
-  const int defaults[8] = {0, 2, 0, 2, 1, 3, 1, 1};
+  const int defaults[8] = {0, 2, 1, 2, 1, 3, 1, 1};
   for (int i = 0; i < 8; ++i) {
     sw[i] = defaults[i];
     const char* e = getenv(kSwitches[i].name);

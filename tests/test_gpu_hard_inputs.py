@@ -242,7 +242,7 @@ def test_large_batch_launch_structures_match_default(monkeypatch, var, base, mod
     same order (one per CU in the pair geometry), so the gradients, scalars and dP0 are
     bit-identical — B=1024, 4 images per ring-walk workgroup.  BA3C_SCALARS_RIDE: the TfDictOp
     scalar reduction in its own launch after the heads (0) or as one workgroup of conv3's
-    weight-gradient launch (1) — the same body, the same scalars."""
+    weight-gradient launch (1, default) — the same body, the same scalars."""
     B = 1024
     rs = np.random.RandomState(83)
     state = dev(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8))
