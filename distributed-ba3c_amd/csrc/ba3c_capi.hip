@@ -1013,7 +1013,14 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
   a.invB = 1.0f / (float)B;
   {
     ProbeScope ps(h, s, BA3C_K_HEADS);
-    hipLaunchKernelGGL(heads_kernel, dim3((B + 3) / 4), dim3(256), 0, s, a);
+    // features per lane unrolled (heads_sample): the smallest instantiation that covers F
+    const int F = a.F;
+    const dim3 g((B + 3) / 4), t(256);
+    if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, FC_SPLIT>), g, t, 0, s, a);
+    else if (F <= 128) hipLaunchKernelGGL((heads_kernel<2, FC_SPLIT>), g, t, 0, s, a);
+    else if (F <= 256) hipLaunchKernelGGL((heads_kernel<4, FC_SPLIT>), g, t, 0, s, a);
+    else if (F <= 512) hipLaunchKernelGGL((heads_kernel<8, FC_SPLIT>), g, t, 0, s, a);
+    else hipLaunchKernelGGL((heads_kernel<0, FC_SPLIT>), g, t, 0, s, a);
   }
   HIP_TRY(hipGetLastError());
   if (train && scalars && !fuse_scalars && defer_scalars) {

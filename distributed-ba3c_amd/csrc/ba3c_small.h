@@ -72,6 +72,12 @@ __device__ __forceinline__ double wave_max_d(double v, int w = 64) { return wave
 // One wave per sample; after the dot products lane a < A owns action a, so the softmax /
 // log / gradient run once per lane (one exp and one log per lane instead of MAXA of each,
 // masked, in every lane) with wave reductions for the sums and maxima.
+// FCH > 0: F <= 64 FCH, a lane's features f = lane + 64 i (i < FCH) are unrolled and EVERY
+// load of the fc1 split-K finish (FCH x NZ chunk values, NZ = fc_split) is issued before the
+// first sum — one global round trip per sample instead of one per 64 features (F=512: eight
+// dependent HBM round trips per wave were most of the B=2048 heads launch).  The sums, their z
+// order and every product are unchanged.  FCH == 0: the runtime loop over f (any F).
+template <int FCH, int NZ>
 __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane) {
   const int A = p.A;
   double acc[MAXA];
@@ -81,7 +87,51 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
   float* hn = p.h + (size_t)n * p.F;
   unsigned long long pos = 0;
   const size_t MN = (size_t)p.B * p.F;
-  for (int f = lane; f < p.F; f += 64) {
+  if constexpr (FCH > 0) {
+    float hv32[FCH];
+    if (p.fcpart) {
+      // unconditional loads (a feature past F re-reads feature F - 1 and is discarded): a
+      // branch around each load made the compiler drain the loads at every join
+      float pz[FCH][NZ];
+#pragma unroll
+      for (int i = 0; i < FCH; ++i) {
+        const int f = min(lane + 64 * i, p.F - 1);
+        const size_t e = (size_t)n * p.F + f;
+#pragma unroll
+        for (int z = 0; z < NZ; ++z) pz[i][z] = p.fcpart[(size_t)z * MN + e];
+      }
+#pragma unroll
+      for (int i = 0; i < FCH; ++i) {
+        const int f = lane + 64 * i;
+        float h32 = pz[i][0];
+#pragma unroll
+        for (int z = 1; z < NZ; ++z) h32 += pz[i][z];
+        if (p.legacy && f < p.F) {
+          const int sidx = f / p.per;
+          h32 = fmaxf(h32 + p.fc_w1[sidx * p.wstride + 1600 * p.per + (f - sidx * p.per)], 0.f);
+          pos += h32 > 0.f;
+        }
+        if (f < p.F) hn[f] = h32;
+        hv32[i] = f < p.F ? h32 : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FCH; ++i) hv32[i] = lane + 64 * i < p.F ? hn[lane + 64 * i] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int f = lane + 64 * i;
+      if (f < p.F) {
+        const double hv = hv32[i];
+        const float* wr = p.piW + (size_t)f * A;
+#pragma unroll
+        for (int a = 0; a < MAXA; ++a)
+          if (a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
+        accv = fma(hv, (double)p.vW[f], accv);
+      }
+    }
+  }
+  for (int f = lane; FCH == 0 && f < p.F; f += 64) {
     float h32;
     if (p.fcpart) {
       const size_t e = (size_t)n * p.F + f;
@@ -160,7 +210,7 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
     }
   }
   float* dhn = p.dh + (size_t)n * p.F;
-  for (int f = lane; f < p.F; f += 64) {
+  auto dh_one = [&](int f) {
     const float* wr = p.piW + (size_t)f * A;
     double g = dV * (double)p.vW[f];
 #pragma unroll
@@ -168,6 +218,13 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
       if (a < A) g = fma(dza[a], (double)wr[a], g);
     if (p.legacy && !(hn[f] > 0.f)) g = 0.0;
     dhn[f] = (float)g;
+  };
+  if constexpr (FCH > 0) {
+#pragma unroll
+    for (int i = 0; i < FCH; ++i)
+      if (lane + 64 * i < p.F) dh_one(lane + 64 * i);
+  } else {
+    for (int f = lane; f < p.F; f += 64) dh_one(f);
   }
   if (lane < NTERMS) {
     double t = 0.0;
@@ -259,10 +316,11 @@ __global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B,
 // (s_waitcnt 0) and the workgroup barriers BEFORE thread 0 increments the counter; the last
 // workgroup reads the words only with agent-scope loads (ld_agent: global_load sc1) after its
 // barrier.  The counter itself is a device atomic.  No step relies on release/acquire ordering.
+template <int FCH, int NZ>
 __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n < p.B) heads_sample(p, n, lane);
+  if (n < p.B) heads_sample<FCH, NZ>(p, n, lane);
   if (p.train && p.scalars) {                 // uniform over the grid
     // terms go out with st_agent and ReLU counts with device atomics; each wave waits for its
     // own stores before the workgroup's arrival is counted (no L2 write-back fence)
