@@ -129,8 +129,10 @@ struct ba3c_handle {
   // count fits one workgroup per CU; its grid-barrier words live in `bar` (device, zeroed at
   // create).  BA3C_FUSED_UPDATE=0: sumsq_kernel + update_kernel.
   bool fused_update = true;
-  // clip_update_kernel's tagged partials (nchunks words) + error flag: device, zeroed at create
+  // clip_update_kernel's tagged partials (nchunks words) + error flag: device, zeroed at create;
+  // clip_range_kernel's (a generation space of their own) follow them
   unsigned long long* utag = nullptr;
+  unsigned long long* ctag = nullptr;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -706,7 +708,8 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   } defer_guard(h);
   // join the side stream and run the deferred reductions of this phase in one launch
   auto finish = [&]() -> int {
-    if (h->pend_scalars) {     // no launch took the deferred scalar reduction
+    if (h->pend_scalars && phase != 1) {   // no launch took the deferred scalar reduction
+      // (phase 1 leaves it pending: conv3's weight-gradient launch in phase 2 takes it)
       const ScalarsJob::Args& sa = h->scalars_args;
       ProbeScope ps(h, s, BA3C_K_SCALARS);
       hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, sa.terms, sa.B, sa.beta, sa.relu, sa.out);
@@ -1152,15 +1155,18 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   }
   tt.chunk0[tt.n] = ch;
   tt.nchunks = ch;
-  // clip_update_kernel's tagged partials + error word (no device: stays null, two-launch apply)
+  // clip_update_kernel's and clip_range_kernel's tagged partials + error words (no device:
+  // stay null, two-launch paths)
   const size_t ubytes = ((size_t)tt.nchunks + 1) * sizeof(unsigned long long);
-  if (hipMalloc(reinterpret_cast<void**>(&h->utag), ubytes) != hipSuccess) {
+  if (hipMalloc(reinterpret_cast<void**>(&h->utag), 2 * ubytes) != hipSuccess) {
     h->utag = nullptr;
     (void)hipGetLastError();
-  } else if (hipMemset(h->utag, 0, ubytes) != hipSuccess) {
+  } else if (hipMemset(h->utag, 0, 2 * ubytes) != hipSuccess) {
     (void)hipFree(h->utag);
     h->utag = nullptr;
     (void)hipGetLastError();
+  } else {
+    h->ctag = h->utag + tt.nchunks + 1;
   }
   *out = h;
   return BA3C_OK;
@@ -1288,7 +1294,7 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
   // heads + loss + its gradient, fc1's split-K finish and (last workgroup) the TfDictOp scalars
   h->pend_scalars = false;
   CHECK(run_heads(h, s, params, w, batch, action, futurereward, entropy_beta, 1.0f, true, nullptr,
-                  nullptr, nullptr, scalars, phase == 0 && h->scalars_ride && h->g6));
+                  nullptr, nullptr, scalars, phase != 2 && h->scalars_ride && h->g6));
   if (h->cfg.channels == 4)
     return run_backward<4>(h, s, params, state, batch, w, grads, phase);
   return run_backward<12>(h, s, params, state, batch, w, grads, phase);
@@ -1301,8 +1307,15 @@ int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* work
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* part = carve(h, workspace, 1, false).sumsq;
   const int c0 = h->table.chunk0[t0], nc = h->table.chunk0[t1] - c0;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, part, c0);
-  hipLaunchKernelGGL(clip_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, (const float*)part, c0);
+  ProbeScope ps(h, s, BA3C_K_CLIP);
+  if (h->ctag && h->fused_update && nc <= h->cus) {
+    // one launch (tagged partials), bit-identical to the two below
+    const UpdateSync us{h->ctag, reinterpret_cast<unsigned int*>(h->ctag + h->table.nchunks)};
+    hipLaunchKernelGGL(clip_range_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, c0, us);
+  } else {
+    hipLaunchKernelGGL(sumsq_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, part, c0);
+    hipLaunchKernelGGL(clip_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, (const float*)part, c0);
+  }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
@@ -1553,9 +1566,10 @@ int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
   if (!h || !flags) return fail(BA3C_ERR_INVALID, "null argument");
   *flags = 0;
   if (!h->utag) return BA3C_OK;
-  uint32_t e = 0;
+  uint32_t e = 0, e2 = 0;
   HIP_TRY(hipMemcpy(&e, h->utag + h->table.nchunks, sizeof(e), hipMemcpyDeviceToHost));
-  *flags = e;
+  if (h->ctag) HIP_TRY(hipMemcpy(&e2, h->ctag + h->table.nchunks, sizeof(e2), hipMemcpyDeviceToHost));
+  *flags = e | (e2 << 1);
   return BA3C_OK;
 }
 

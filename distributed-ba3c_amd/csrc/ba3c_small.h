@@ -808,6 +808,54 @@ __global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, co
 }
 
 // ---------------------------------------------------------------------------------------
+// clip_by_average_norm over a tensor-aligned chunk range [cbase, cbase + gridDim.x) in ONE
+// launch (the data-parallel step clips each gradient bucket before its all-reduce): the
+// sumsq_kernel + clip_kernel pair with clip_update_kernel's tagged-partials hand-off — phase 1
+// publishes the chunk's sum of squares in sumsq_kernel's order, phase 2 waits for its tensor's
+// chunks and scales in clip_kernel's arithmetic, bit for bit.  Its tags are a generation space
+// of their own (a range launch advances only its chunks).  All chunks of the range co-resident.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) clip_range_kernel(float* __restrict__ g, const TensorTable tt, int cbase,
+                                                         const UpdateSync us) {
+  __shared__ float red[4];
+  __shared__ float fsh;
+  const int b = blockIdx.x + cbase;
+  const int lane = threadIdx.x & 63;
+  const unsigned gen = (unsigned)(ld_agent_u64(us.tag + b) >> 32) + 1u;
+  const int t = table_find(tt, b);
+  const int c = b - tt.chunk0[t];
+  const int beg = c * UPD_CHUNK;
+  const int end = min(tt.numel[t], beg + UPD_CHUNK);
+  float* gt = g + tt.off[t];
+  constexpr int PER = UPD_CHUNK / 256;
+  float gv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = beg + threadIdx.x + 256 * j;
+    gv[j] = i < end ? gt[i] : 0.f;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (beg + (int)threadIdx.x + 256 * j < end) ss = fmaf(gv[j], gv[j], ss);
+  ss = block_sum_256(ss, red);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(us.tag + b, ((unsigned long long)gen << 32) | __float_as_uint(ss), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 64) {
+    const float sum = wave_sum_f(wait_partials(us, tt.chunk0[t], tt.chunk0[t + 1], gen, lane));
+    if (lane == 0) fsh = fminf(rsqrtf(sum) * (float)tt.numel[t], 10.0f);
+  }
+  __syncthreads();
+  const float f = fsh;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = beg + threadIdx.x + 256 * j;
+    if (i < end) gt[i] = (gv[j] * 0.1f) * f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // numpy RandomState.choice(A, p=p) given its draw u:  cdf = cumsum(double(p)); cdf /= cdf[-1];
 // a = searchsorted(cdf, u, 'right').  flag bits: 1 non-finite p (train.py:381), 2 |sum-1| >
 // sqrt(eps_f32) ("probabilities do not sum to 1"), 4 negative p.

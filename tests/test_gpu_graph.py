@@ -190,3 +190,39 @@ def test_two_phase_backward_equals_one_pass(B):
         else:
             assert torch.equal(eng.grads[o:o + n], ref[o:o + n]), name
     assert torch.equal(sc1, sc)
+
+
+def test_one_launch_bucket_clip_matches_two_launch_clip(monkeypatch):
+    """ba3c_clip_grads_range (the data-parallel step's per-bucket clip, train.py:329-330 per
+    replica) runs as ONE launch with tagged partials (clip_range_kernel); BA3C_FUSED_UPDATE=0
+    keeps sumsq + clip launches.  Same gradients in, bit-identical clipped buckets out, over
+    repeated calls on both buckets (the tags advance per chunk), and no wait gave up."""
+    from ba3c_amd.engine import Ba3cEngine
+    B = 32
+    rs = np.random.RandomState(41)
+    state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    params = O.init_params(512, 1, 4, seed=8, dtype=np.float32)
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("BA3C_FUSED_UPDATE", fused)
+        eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=B)
+        eng.load_params(params)
+        tb, _ = eng.bucket_split()
+        nt = len(eng.layout)
+        got = []
+        for step in range(3):
+            eng.train_grads(state, action, R)
+            eng.clip_grads_range(tb, nt)
+            eng.clip_grads_range(0, tb)
+            got.append(eng.grads.clone())
+            eng.grads.mul_(1.5 + step)                   # a second clip of other values
+            eng.clip_grads_range(0, tb)
+            got.append(eng.grads.clone())
+        torch.cuda.synchronize()
+        assert eng.device_errors() == 0
+        out.append(got)
+        del eng
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
