@@ -357,19 +357,50 @@ class SyncReplicasOptimizer(object):
             self._comm = torch.cuda.Stream(device=device)
         return self._comm
 
-    def aggregate_bucket_async(self, engine, t0, t1, off0, off1, marks=None):
-        """Clip tensors [t0, t1) and start the RCCL sum of flat range [off0, off1) on the
-        exchange stream; returns the work handle (None without a process group).  `marks`:
-        (begin, end) timing events recorded on the exchange stream around the sum."""
+    # RCCL driven directly (rccl.py) for the bucket sums on a 'nccl' group; BA3C_DIRECT_RCCL=0
+    # keeps torch's collective (its own stream, joined with events)
+    _rccl = None
+
+    def direct_rccl(self, device):
+        """The direct RCCL communicator of this group (created on first use, collectively), or
+        None on a gloo group or with BA3C_DIRECT_RCCL=0."""
+        flag = os.environ.get("BA3C_DIRECT_RCCL", "1")
+        if flag not in ("0", "1"):
+            raise ValueError("BA3C_DIRECT_RCCL must be 0 or 1 (got %r)" % flag)
+        if flag == "0" or dist.get_backend(self.group) != "nccl":
+            return None
+        if self._rccl is None:
+            from .rccl import RcclComm
+            self._rccl = RcclComm(self.group, device)
+        return self._rccl
+
+    def aggregate_bucket_async(self, engine, t0, t1, off0, off1, marks=None, last=False):
+        """Clip tensors [t0, t1) and start the RCCL sum of flat range [off0, off1); returns
+        the work handle (None when there is nothing to join).  The sum runs on the exchange
+        stream, except the `last` bucket's on a direct-RCCL group: the update waits for it
+        next, so it is enqueued on the current stream itself.  `marks`: (ready, begin, end)
+        timing events — `ready` on the current stream after the clip, begin / end around the
+        sum on the stream that runs it."""
         engine.clip_grads_range(t0, t1)
+        ready, begin, end = marks if marks is not None else (None, None, None)
+        cur = torch.cuda.current_stream(engine.grads.device) if engine.grads.is_cuda else None
+        if ready is not None:
+            ready.record(cur)
         if not self.distributed:
             return None
         buf = engine.grads[off0:off1]
         if not buf.is_cuda:
             return self._all_reduce(buf, async_op=True)
+        rccl = self.direct_rccl(buf.device)
+        if rccl is not None and last:
+            if begin is not None:
+                begin.record(cur)
+            rccl.all_reduce_sum(buf, cur)
+            if end is not None:
+                end.record(cur)
+            return None
         comm = self.comm_stream(buf.device)
-        comm.wait_stream(torch.cuda.current_stream(buf.device))
-        begin, end = marks if marks is not None else (None, None)
+        comm.wait_stream(cur)
         with torch.cuda.stream(comm):
             if begin is not None:
                 begin.record(comm)
@@ -377,8 +408,11 @@ class SyncReplicasOptimizer(object):
                 host = buf.cpu()              # host-staged (gloo): waits for the clip
                 work = dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                 return _StagedWork(work, host, buf, stream=comm, end=end)
-            work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            work.wait()                       # RCCL: `comm` waits for the collective's stream
+            if rccl is not None:
+                rccl.all_reduce_sum(buf, comm)
+            else:
+                work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                work.wait()                   # `comm` waits for the collective's stream
             if end is not None:
                 end.record(comm)
         return _StreamJoin(comm)

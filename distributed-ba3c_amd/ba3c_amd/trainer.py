@@ -140,16 +140,17 @@ class Ba3cTrainer(object):
         m.train_phase = 1
         try:
             m.build_graph(inputs)
-            work = opt.aggregate_bucket_async(eng, tb, nt, off, total,
-                                              marks=tl and (tl["fc1_ar_begin"], tl["fc1_ar_end"]))
-            mark("fc1_ready")     # after the bucket's clip (the sum may start from here)
+            # fc1_ready / conv_ready: after the bucket's clip (its sum may start from there)
+            work = opt.aggregate_bucket_async(
+                eng, tb, nt, off, total,
+                marks=tl and (tl["fc1_ready"], tl["fc1_ar_begin"], tl["fc1_ar_end"]))
             m.train_phase = 2
             m.build_graph(inputs)
         finally:
             m.train_phase = 0
-        work2 = opt.aggregate_bucket_async(eng, 0, tb, 0, off,
-                                           marks=tl and (tl["conv_ar_begin"], tl["conv_ar_end"]))
-        mark("conv_ready")
+        work2 = opt.aggregate_bucket_async(
+            eng, 0, tb, 0, off, last=True,
+            marks=tl and (tl["conv_ready"], tl["conv_ar_begin"], tl["conv_ar_end"]))
         for w in (work, work2):
             if w is not None:
                 w.wait()

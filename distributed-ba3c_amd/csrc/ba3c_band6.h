@@ -698,13 +698,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
 struct WPrep6Args {
   WPrepArgs jobs;
   uint16_t* wt6;
-  int off[4];              // fp32 offset of job i; its splits start at NS * off[i]
+  int off[6];              // fp32 offset of job i; its splits start at NS * off[i]
   const float* w0;         // conv0/W (null: no conv0 job)
   uint4* wb0;
   unsigned long long* relu;  // training: ReLU-count slots zeroed here (no separate memset)
   uint32_t* amax;          // max-|x| slots zeroed here (n_amax words; may be null)
   int n_amax;
-  int* wexp;               // [5]: weight scale exponents of jobs 0..3 and conv0
+  int* wexp;               // [8]: weight scale exponents of jobs 0..5 and conv0 (slot 7)
 };
 
 // (bx, by, gx): blockIdx.x, blockIdx.y, gridDim.x of a plain launch; red4: 4 floats of LDS
@@ -718,7 +718,7 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
   }
   if (y == a.jobs.njobs) {
     const int k = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, red4)));
-    if (bx == 0 && threadIdx.x == 0) a.wexp[4] = k;
+    if (bx == 0 && threadIdx.x == 0) a.wexp[7] = k;
     conv0s_wprep_one(a.w0, a.wb0, bx * 256 + threadIdx.x, k);
     return;
   }

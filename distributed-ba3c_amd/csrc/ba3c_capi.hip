@@ -18,6 +18,7 @@
 #include "../../include/ba3c.h"
 #include "ba3c_band6.h"
 #include "ba3c_conv.h"
+#include "ba3c_conv3.h"
 #include "ba3c_gemm6.h"
 #include "ba3c_launch.h"
 #include "ba3c_multi.h"
@@ -213,9 +214,12 @@ static_assert(W6W_P <= WG_P1, "conv1 partial slabs: the allocation covers WG_P1 
 inline bool conv1_pair_geometry(int B, int cus) { return B >= 2 * W6W_MIN_B && B % cus == 0 && cus <= WG_P1; }
 inline int conv1_w6w_p(int B, int cus) { return conv1_pair_geometry(B, cus) ? cus : std::min(W6W_P, B); }
 constexpr int FW_P0S = 512;   // conv0s_fwd_kernel: persistent, two workgroups per CU
+constexpr int C3W_P = 256;    // conv3_wgrad_kernel: one 512-thread workgroup (and slab) per CU, at most
+inline int conv3_wgrad_p(int B, int cus) { return std::min(B, std::min(C3W_P, cus)); }
 constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
-constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C1D = WT_C2F + 800 * 64,
-              WT_C2D = WT_C1D + 800 * 32, WT_C0F = WT_C2D + 1600 * 32,
+constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C3F = WT_C2F + 800 * 64,
+              WT_C1D = WT_C3F + 576 * 64, WT_C2D = WT_C1D + 800 * 32, WT_C3D = WT_C2D + 1600 * 32,
+              WT_C0F = WT_C3D + 576 * 64,
               WT_C0S = WT_C0F + 32 * Conv0Geom::KDIM,            // uint4 [Conv0S::WB_U4]
               WT_TOTAL = WT_C0S + 4 * Conv0S::WB_U4;
 
@@ -228,12 +232,15 @@ struct Workspace {
   uint8_t *c0, *c1, *c2;
   unsigned long long* relu;
   uint32_t* amax;  // [AMAX_N][1 + max_batch]: max |x| of split operands (global, per image)
-  int* wexp;       // [8]: weight scale exponents (wprep jobs 0..3, conv0 = 4)
+  int* wexp;       // [8]: weight scale exponents (wprep jobs WJ_*, conv0 = WX_CONV0)
   size_t bytes;
   uint32_t* am(int t, const ba3c_handle* h) const { return amax + (size_t)t * (1 + h->cfg.max_batch); }
 };
 // max-|x| slot arrays (ba3c_split.h, fp16 family)
-enum { AM_P0 = 0, AM_P1 = 1, AM_DP0 = 2, AM_DP1 = 3, AM_DP2 = 4, AMAX_N = 5 };
+enum { AM_P0 = 0, AM_P1 = 1, AM_DP0 = 2, AM_DP1 = 3, AM_DP2 = 4, AM_P2 = 5, AM_DY3 = 6, AMAX_N = 7 };
+// weight-preparation jobs (forward copies first: inference prepares only those) and the
+// index of each one's scale exponent in Workspace::wexp
+enum { WJ_C1F = 0, WJ_C2F = 1, WJ_C3F = 2, WJ_C1D = 3, WJ_C2D = 4, WJ_C3D = 5, WJ_N = 6, WJ_FWD = 3, WX_CONV0 = 7 };
 
 struct WgradPlan {
   int M, N, K, S, kchunk, mt, nt;
@@ -262,6 +269,12 @@ constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
 constexpr int FC_KCHUNK = 160, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;
 static_assert(FC_SPLIT <= FC_SPLIT_MAX, "heads kernel finishes at most FC_SPLIT_MAX chunks");
 static_assert(FC_KCHUNK % GEMM_BK == 0, "k-chunk of whole k-tiles");
+// fc1's forward with its FC_SPLIT chunks summed inside each 64 x 64 workgroup (gemm6_body's
+// chunked K: no partial slabs, one slab for the heads kernel) where those tiles alone fill the
+// chip; the chunks and their order are the split-K launch's, so h is bit-identical either way
+inline bool fc_chunk_acc(const ba3c_handle* h, int B) {
+  return h->g6 && ((B + 63) / 64) * ((h->cfg.fc_neurons + 63) / 64) >= h->cus;
+}
 
 // conv0's weight gradient runs on the main stream while the other weight gradients run on
 // the side stream, so its split-K partials get a region of their own
@@ -283,7 +296,7 @@ PartialSizes partial_sizes(const ba3c_handle* h, int B) {
   PartialSizes p;
   p.heads = sz(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
   p.fc1 = sz(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
-  p.conv3 = sz(plan_wgrad(576, 64, B * 25, 128, 64));
+  p.conv3 = std::max(sz(plan_wgrad(576, 64, B * 25, 128, 64)), (size_t)C3W_P * 576 * 64);
   p.conv2 = std::max(sz(plan_wgrad(800, 64, B * 196, 128, 64)), (size_t)W6_P2 * Lay::W2::M * Lay::W2::COUT);
   p.conv1 = std::max(sz(plan_wgrad(800, 32, B * 1296, 128, 32)), (size_t)WG_P1 * Lay::W1::M * Lay::W1::COUT);
   return p;
@@ -509,16 +522,19 @@ int reduce_wgrad6(ba3c_handle* h, hipStream_t s, const Wg6Args& a, int P, float*
 WPrep6Args wprep6_args(ba3c_handle* h, const float* prm, const Workspace& w, bool train) {
   const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
   const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
+  const float* W3 = prm + h->tensors[h->idx_conv[3]].offset;
   WPrep6Args pa{};
   WPrepArgs& a = pa.jobs;
-  a.job[0] = WPrepJob{W1, w.wt + WT_C1F, 5, 5, 32, 32, 0, 800 * 32};
-  a.job[1] = WPrepJob{W2, w.wt + WT_C2F, 5, 5, 32, 64, 0, 800 * 64};
-  a.job[2] = WPrepJob{W1, w.wt + WT_C1D, 5, 5, 32, 32, 1, 800 * 32};
-  a.job[3] = WPrepJob{W2, w.wt + WT_C2D, 5, 5, 32, 64, 1, 1600 * 32};
-  a.njobs = train ? 4 : 2;
+  a.job[WJ_C1F] = WPrepJob{W1, w.wt + WT_C1F, 5, 5, 32, 32, 0, 800 * 32};
+  a.job[WJ_C2F] = WPrepJob{W2, w.wt + WT_C2F, 5, 5, 32, 64, 0, 800 * 64};
+  a.job[WJ_C3F] = WPrepJob{W3, w.wt + WT_C3F, 3, 3, 64, 64, 0, 576 * 64};
+  a.job[WJ_C1D] = WPrepJob{W1, w.wt + WT_C1D, 5, 5, 32, 32, 1, 800 * 32};
+  a.job[WJ_C2D] = WPrepJob{W2, w.wt + WT_C2D, 5, 5, 32, 64, 1, 1600 * 32};
+  a.job[WJ_C3D] = WPrepJob{W3, w.wt + WT_C3D, 3, 3, 64, 64, 1, 576 * 64};
+  a.njobs = train ? WJ_N : WJ_FWD;
   pa.wt6 = w.wt6;
-  const int offs[4] = {WT_C1F, WT_C2F, WT_C1D, WT_C2D};
-  for (int j = 0; j < 4; ++j) pa.off[j] = offs[j];
+  const int offs[WJ_N] = {WT_C1F, WT_C2F, WT_C3F, WT_C1D, WT_C2D, WT_C3D};
+  for (int j = 0; j < WJ_N; ++j) pa.off[j] = offs[j];
   pa.w0 = prm + h->tensors[h->idx_conv[0]].offset;
   pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
   pa.relu = train ? w.relu : nullptr;
@@ -542,7 +558,7 @@ int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, con
   hipLaunchKernelGGL(wprep6_kernel, dim3(64, 1), dim3(256), 0, s, first);
   HIP_TRY(hipGetLastError());
   const Conv0SArgs sa{state, reinterpret_cast<const uint4*>(w.wt + WT_C0S), w.p0, train ? w.c0 : nullptr,
-                      train ? w.relu : nullptr, B, w.wexp + 4, w.am(AM_P0, h)};
+                      train ? w.relu : nullptr, B, w.wexp + WX_CONV0, w.am(AM_P0, h)};
   ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
   return launch_multi<false, Conv0SJob, WPrep6Job>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)), rest,
                                                   dim3(64, rest.jobs.njobs));
@@ -561,10 +577,23 @@ int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspac
 
 int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a, const Workspace& w) {
   const Conv0SArgs sa{reinterpret_cast<const uint8_t*>(a.src), reinterpret_cast<const uint4*>(w.wt + WT_C0S),
-                      a.out, a.out_code, a.relu_count, a.batch, w.wexp + 4, w.am(AM_P0, h)};
+                      a.out, a.out_code, a.relu_count, a.batch, w.wexp + WX_CONV0, w.am(AM_P0, h)};
   ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
   const dim3 grid(std::min(FW_P0S, a.batch * Conv0S::NBANDS));
   HIP_TRY(launch_conv0s_fwd(grid, s, sa));   // ba3c_conv0.hip
+  return BA3C_OK;
+}
+
+// conv3 forward / input gradient: persistent whole-image workgroups, two per CU (ba3c_conv3.h)
+template <bool DG>
+int launch_conv3(ba3c_handle* h, hipStream_t s, int kid, const Conv3Args& a) {
+  if (a.batch <= 0) return BA3C_OK;
+  const dim3 grid(std::min(a.batch, 2 * h->cus));
+  {
+    ProbeScope ps(h, s, kid);
+    hipLaunchKernelGGL(conv3_band_kernel<DG>, grid, dim3(256), 0, s, a);
+  }
+  HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
 
@@ -585,7 +614,7 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   uint8_t* c0 = train ? w.c0 : nullptr;
   uint8_t* c1 = train ? w.c1 : nullptr;
   uint8_t* c2 = train ? w.c2 : nullptr;
-  const SplitIO io1{AM_P0, 0, AM_P1}, io2{AM_P1, 1, -1};
+  const SplitIO io1{AM_P0, WJ_C1F, AM_P1}, io2{AM_P1, WJ_C2F, AM_P2};
   if (!h->band) {
     ConvFwd<true, 84, 84, CH, 16, 5, 5, 32, 0> cv0{state, W0, w.p0, c0, rc, 1.0f / 255.0f, B * 6400, 32, 25 * CH, 0};
     CHECK((launch_gemm<128, 32, 4, 1>(h, s, BA3C_K_CONV0_FWD, cv0, 1)));
@@ -617,10 +646,16 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
     else
       CHECK(launch_band6<typename LY::C2F>(h, s, BA3C_K_CONV2_FWD, a2, w, WT_C2F, io2));
   }
-  ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
-  // K = 576 in two halves of 9 k-tiles summed in the workgroup (KS = 2) at every batch, so
-  // each output's rounding is the same whatever batch it runs in
-  CHECK((launch_gemm<64, 64, 2, 2, decltype(c3), 2>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
+  if (h->band) {
+    // whole-image workgroups at every batch: an image's a3 does not depend on its batch
+    CHECK(launch_conv3<false>(h, s, BA3C_K_CONV3_FWD, Conv3Args{w.p2, w.wt6 + 2 * (size_t)WT_C3F, w.wexp + WJ_C3F,
+                                                                  w.a3, rc, nullptr, B, nullptr}));
+  } else {
+    ConvFwd<false, 7, 7, 64, 64, 3, 3, 64, 2> c3{w.p2, W3, w.a3, nullptr, rc, 1.0f, B * 25, 64, 576, 0};
+    // K = 576 in two halves of 9 k-tiles summed in the workgroup (KS = 2) at every batch, so
+    // each output's rounding is the same whatever batch it runs in
+    CHECK((launch_gemm<64, 64, 2, 2, decltype(c3), 2>(h, s, BA3C_K_CONV3_FWD, c3, 1)));
+  }
   // split-K: K = 1600 in FC_SPLIT fixed chunks (a 128x64 tile over all of K is one
   // workgroup's 50 serial k-tiles: latency-bound at any batch); the chunk sums (+ legacy bias,
   // ReLU, count) are finished inside the heads kernel (run_heads), which reads them anyway
@@ -629,7 +664,12 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   {
     ProbeScope ps(h, s, BA3C_K_FC1_FWD);
     const dim3 grid((B + 127) / 128, (F + 63) / 64, FC_SPLIT);
-    if (h->g6 && B <= 64)   // 64-row tiles: same per-row K order, half the dead rows staged
+    if (fc_chunk_acc(h, B)) {
+      fc.kchunk = 0;
+      fc.acc_tiles = FC_KCHUNK / GEMM_BK;
+      hipLaunchKernelGGL((gemm6_kernel<64, 64, 2, 2, FcFwd, 4>), dim3((B + 63) / 64, (F + 63) / 64, 1),
+                         dim3(GEMM_THREADS), 0, s, fc);
+    } else if (h->g6 && B <= 64)   // 64-row tiles: same per-row K order, half the dead rows staged
       hipLaunchKernelGGL((gemm6_kernel<64, 64, 2, 2, FcFwd, 4>), dim3((B + 63) / 64, grid.y, grid.z),
                          dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
@@ -808,6 +848,28 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, decltype(d), 4, 2>, Gemm6Job<128, 64, 4, 1, decltype(g), 4, 2>,
                           NoJob, true>(s, d, gd, g, gw, 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
       h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_CONV3_WGRAD;
+    } else if (h->band) {
+      // input gradient first: it publishes dY3's per-image maxima, the weight gradient's scale
+      // (both on `s`, whatever the side-stream setting); the deferred TfDictOp reduction rides
+      // on it as one extra workgroup
+      const Conv3Args da{w.dy3, w.wt6 + 2 * (size_t)WT_C3D, w.wexp + WJ_C3D, w.dp2, nullptr,
+                         w.am(AM_DP2, h), B, w.am(AM_DY3, h)};
+      if (big && h->pend_scalars) {
+        CHECK((launch_multi<true, Conv3DJob, ScalarsJob>(s, da, dim3(std::min(B, 2 * h->cus)), h->scalars_args,
+                                                          dim3(1), 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
+        h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_SCALARS;   // the reduction rode on this launch
+        h->pend_scalars = false;
+      } else {
+        CHECK(launch_conv3<true>(h, s, BA3C_K_CONV3_DGRAD, da));
+      }
+      const int gx = conv3_wgrad_p(B, h->cus);
+      {
+        ProbeScope ps(h, s, BA3C_K_CONV3_WGRAD);
+        hipLaunchKernelGGL(conv3_wgrad_kernel, dim3(gx), dim3(512), 0, s,
+                           Conv3WArgs{w.p2, w.dy3, w.part_3, B, w.am(AM_P2, h), w.am(AM_DY3, h)});
+      }
+      HIP_TRY(hipGetLastError());
+      pl.S = gx;   // one slab per workgroup
     } else {
       const bool deep = (int)(gw.x * gw.y * gw.z) < h->cus;   // launch_gemm's ring depth
       if (big && h->pend_scalars && h->g6 && !deep) {
@@ -827,7 +889,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     const Wg6Args wa{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)};
     const dim3 wg = wgrad6_grid<typename LY::W2>(W6_P2, B);
     const Band6Args da = band6_args<typename LY::C2DS>(h, BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B},
-                                                      w, WT_C2D, SplitIO{AM_DP2, 3, AM_DP1});
+                                                      w, WT_C2D, SplitIO{AM_DP2, WJ_C2D, AM_DP1});
     CHECK((launch_multi<true, Band6Job<typename LY::C2DS>, Wg6Job<typename LY::W2>>(
         s, da, dim3(B * LY::C2DS::G::NBANDS), wa, wg)));
     h->merged[BA3C_K_CONV2_DGRAD] |= 1u << BA3C_K_CONV2_WGRAD;
@@ -836,7 +898,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     const Wg6Args wa{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)};
     const dim3 wg = wgrad6_grid<typename LY::W2>(W6_P2, B);
     const Band6Args da = band6_args<typename LY::C2D>(h, BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B},
-                                                     w, WT_C2D, SplitIO{AM_DP2, 3, AM_DP1});
+                                                     w, WT_C2D, SplitIO{AM_DP2, WJ_C2D, AM_DP1});
     CHECK((launch_multi<true, Band6Job<typename LY::C2D>, Wg6Job<typename LY::W2>>(
         s, da, dim3(B * LY::C2D::G::NBANDS), wa, wg, 0, dim3(0, 1, 1), h, BA3C_K_CONV2_DGRAD)));
     h->merged[BA3C_K_CONV2_DGRAD] |= 1u << BA3C_K_CONV2_WGRAD;
@@ -854,7 +916,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
     if (h->band) {
       const BandArgs ba{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B};
-      const SplitIO io{AM_DP2, 3, AM_DP1};
+      const SplitIO io{AM_DP2, WJ_C2D, AM_DP1};
       if (B <= SMALL_B)
         CHECK(launch_band6<typename LY::C2DS>(h, s, BA3C_K_CONV2_DGRAD, ba, w, WT_C2D, io));
       else
@@ -870,7 +932,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
     const dim3 wg = wgrad6_grid<typename LY::W1>(conv1_wgrad_p(B), B);
     const Band6Args da = band6_args<typename LY::C1D>(h, BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B},
-                                                     w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0});
+                                                     w, WT_C1D, SplitIO{AM_DP1, WJ_C1D, AM_DP0});
     CHECK((launch_multi<true, Band6Job<typename LY::C1D>, Wg6Job<typename LY::W1>>(
         s, da, dim3(B * LY::C1D::G::NBANDS), wa, wg)));
     h->merged[BA3C_K_CONV1_DGRAD] |= 1u << BA3C_K_CONV1_WGRAD;
@@ -888,7 +950,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
         using GW = typename LY::W1W;
         const Wg6Args wa{w.p0, w.dp1, w.c1, w.part_1, B, w.am(AM_P0, h), w.am(AM_DP1, h)};
         const Band6Args da = band6_args<typename LY::C1D>(h, BandArgs{w.dp1, w.c1, w.wt + WT_C1D, w.dp0, nullptr, nullptr, B},
-                                                         w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0});
+                                                         w, WT_C1D, SplitIO{AM_DP1, WJ_C1D, AM_DP0});
         CHECK((launch_multi<true, Band6RJob<typename LY::C1D>, Wg6WJob<GW>>(
             s, da, dim3(h->cus), wa, dim3(h->cus), 0, dim3(0, 1, 1), h, BA3C_K_CONV1_DGRAD)));
         h->merged[BA3C_K_CONV1_DGRAD] |= 1u << BA3C_K_CONV1_WGRAD;
@@ -923,7 +985,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       // both gradients ran in the multi-job launch above
     } else if (h->band) {
       const BandArgs ba{w.dp1, w.c1, nullptr, w.dp0, nullptr, nullptr, B};
-      CHECK(launch_band6<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, 2, AM_DP0},
+      CHECK(launch_band6<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, WJ_C1D, AM_DP0},
                                            true));
     } else {
       ConvDgrad<40, 40, 32, 5, 5, 32, true> d{w.dp1, w.c1, W1c, w.dp0, B * 1600, 32, 800, 0};
@@ -982,7 +1044,7 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
               bool defer_scalars = false) {
   HeadsArgs a{};
   a.fcpart = w.fcpart;
-  a.fc_split = FC_SPLIT;
+  a.fc_split = fc_chunk_acc(h, B) ? 1 : FC_SPLIT;
   a.per = h->per;
   a.wstride = h->wstride;
   a.fc_w1 = prm + h->tensors[h->idx_fc1].offset;
@@ -1019,7 +1081,13 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
     // features per lane unrolled (heads_sample): the smallest instantiation that covers F
     const int F = a.F;
     const dim3 g((B + 3) / 4), t(256);
-    if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, FC_SPLIT>), g, t, 0, s, a);
+    if (a.fc_split == 1) {   // fc1's chunks already summed (fc_chunk_acc)
+      if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, 1>), g, t, 0, s, a);
+      else if (F <= 128) hipLaunchKernelGGL((heads_kernel<2, 1>), g, t, 0, s, a);
+      else if (F <= 256) hipLaunchKernelGGL((heads_kernel<4, 1>), g, t, 0, s, a);
+      else if (F <= 512) hipLaunchKernelGGL((heads_kernel<8, 1>), g, t, 0, s, a);
+      else hipLaunchKernelGGL((heads_kernel<0, 1>), g, t, 0, s, a);
+    } else if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 128) hipLaunchKernelGGL((heads_kernel<2, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 256) hipLaunchKernelGGL((heads_kernel<4, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 512) hipLaunchKernelGGL((heads_kernel<8, FC_SPLIT>), g, t, 0, s, a);
@@ -1530,9 +1598,11 @@ int ba3c_kernel_split(const ba3c_handle* h, int32_t kid) {
     case BA3C_K_CONV2_DGRAD:
     case BA3C_K_CONV1_WGRAD:
     case BA3C_K_CONV2_WGRAD: return h->band ? 3 : 1;
+    // conv3: whole-image fp16x3 kernels (the backward ones above OVERLAP_B; below it the
+    // multi-job bf16x6 GEMMs)
     case BA3C_K_CONV3_FWD:
     case BA3C_K_CONV3_DGRAD:
-    case BA3C_K_CONV3_WGRAD:
+    case BA3C_K_CONV3_WGRAD: return h->band ? 3 : (h->g6 ? 6 : 1);
     case BA3C_K_FC1_FWD:
     case BA3C_K_FC1_DGRAD:
     case BA3C_K_FC1_WGRAD:
@@ -1556,7 +1626,8 @@ int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {
   if (sp <= 1) return sp;
   const bool band_split = kid == BA3C_K_CONV0_FWD || kid == BA3C_K_CONV0_WGRAD || kid == BA3C_K_CONV1_FWD ||
                           kid == BA3C_K_CONV2_FWD || kid == BA3C_K_CONV1_DGRAD || kid == BA3C_K_CONV2_DGRAD ||
-                          kid == BA3C_K_CONV1_WGRAD || kid == BA3C_K_CONV2_WGRAD;
+                          kid == BA3C_K_CONV1_WGRAD || kid == BA3C_K_CONV2_WGRAD ||
+                          kid == BA3C_K_CONV3_FWD || kid == BA3C_K_CONV3_DGRAD || kid == BA3C_K_CONV3_WGRAD;
   if (kid == BA3C_K_CONV0_FWD || kid == BA3C_K_CONV0_WGRAD)
     if (!(h->band && h->cfg.channels == 4)) return 3;
   return band_split ? 2 : 3;

@@ -74,7 +74,7 @@ struct WPrepJob {
   int KH, KW, CI, CO, dgrad, n;   // n = total elements
 };
 struct WPrepArgs {
-  WPrepJob job[4];
+  WPrepJob job[6];
   int njobs;
 };
 

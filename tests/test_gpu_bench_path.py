@@ -138,16 +138,20 @@ def _free_port():
     return p
 
 
-def test_sync_replicas_rccl_allreduce_world1_equals_single_replica_step():
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_sync_replicas_rccl_allreduce_world1_equals_single_replica_step(monkeypatch, direct):
     """SyncReplicasOptimizer inside a world-size-1 'nccl' (RCCL) process group: the clip, the
     RCCL all-reduce on the HIP stream and the grad_scale update run for real, and the result
-    equals the single-replica fused-clip step bit for bit."""
+    equals the single-replica fused-clip step bit for bit — with the bucket sums driven
+    through RCCL directly (rccl.py, the default) and through torch's collective."""
     import torch.distributed as dist
     from ba3c_amd.model import Model
     from ba3c_amd.optimizer import AdamOptimizer, SyncReplicasOptimizer
     from ba3c_amd.trainer import Ba3cTrainer, TrainConfig
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    monkeypatch.setenv("BA3C_DIRECT_RCCL", direct)
     batches = [tuple(dev(x) for x in b) for b in _replica_batches(3, 16, 900)]
+    opts = []
 
     def run(sync):
         m = Model(num_actions=4, fc_neurons=128, fc_splits=4, batch_size=16, max_batch=16, seed=9)
@@ -155,6 +159,7 @@ def test_sync_replicas_rccl_allreduce_world1_equals_single_replica_step():
         if sync:
             opt = SyncReplicasOptimizer(opt, replicas_to_aggregate=1, total_num_replicas=1)
             assert opt.distributed
+            opts.append(opt)
         tr = Ba3cTrainer(TrainConfig(model=m, optimizer=opt))
         for b in batches:
             tr.train_step(*b)
@@ -166,6 +171,9 @@ def test_sync_replicas_rccl_allreduce_world1_equals_single_replica_step():
                             world_size=1, device_id=torch.device("cuda", torch.cuda.current_device()))
     try:
         got = run(True)
+        assert (opts[0]._rccl is not None) == (direct == "1")
+        if opts[0]._rccl is not None:
+            opts[0]._rccl.close()
     finally:
         dist.destroy_process_group()
     np.testing.assert_array_equal(got, ref)

@@ -1,0 +1,53 @@
+"""The bench workload itself (B=2048, F=512, S=1) through the default kernels against the
+fp32-MFMA GEMM engine (BA3C_GENERIC=1, an independent fp32 implementation of every layer) on the
+same weights and frames: every gradient within the oracle tolerance (1e-4 normwise), the forward
+activations and TfDictOp scalars within 1e-5.  The fp64 oracle is too slow at this size; the
+B=160 / B=512 oracle tests hold both engines to it, and this closes the chain at the size the
+bench runs (4 images per persistent conv3 / ring-walk workgroup, one conv3 weight-gradient slab
+per CU).  Decisions (argmax codes, ReLU signs) may differ on fp32 near-ties, so the check allows
+a few positions of difference and compares the gradients normwise."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ba3c_oracle as O
+from test_gpu_parity import rel
+
+pytestmark = pytest.mark.gpu
+
+B = 2048
+
+
+def _run(monkeypatch, generic, params, state, action, R):
+    from ba3c_amd.engine import Ba3cEngine
+    monkeypatch.setenv("BA3C_GENERIC", "1" if generic else "0")
+    eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=B)
+    eng.load_params(params)
+    sc = eng.train_grads(state, action, R, entropy_beta=0.01)
+    out = {k: v.astype(np.float64) for k, v in eng.state_dict(eng.grads).items()}
+    acts = {n: eng.workspace_tensor(n, B).cpu().numpy().astype(np.float64) for n in ("p2", "a3", "dp2")}
+    codes = {n: eng.workspace_tensor(n, B).cpu().numpy() for n in ("c0", "c1", "c2")}
+    s = sc.cpu().numpy().astype(np.float64)
+    del eng
+    torch.cuda.synchronize()
+    return out, acts, codes, s
+
+
+def test_bench_workload_matches_generic_fp32_engine(monkeypatch):
+    rs = np.random.RandomState(2048)
+    params = O.init_params(512, 1, 4, seed=21, dtype=np.float32)
+    state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    g_def, a_def, c_def, s_def = _run(monkeypatch, False, params, state, action, R)
+    g_gen, a_gen, c_gen, s_gen = _run(monkeypatch, True, params, state, action, R)
+    for n in c_def:
+        assert np.mean(c_def[n] != c_gen[n]) < 1e-4, n
+    for n in ("p2", "a3"):
+        assert rel(a_def[n], a_gen[n]) < 1e-5, (n, rel(a_def[n], a_gen[n]))
+    assert rel(a_def["dp2"], a_gen["dp2"]) < 1e-4
+    for k in g_gen:
+        e = rel(g_def[k], g_gen[k])
+        assert e < 1e-4, (k, e)
+    for i in range(7):
+        assert abs(s_def[i] - s_gen[i]) <= 1e-4 * max(1.0, abs(s_gen[i])), (i, s_def[i], s_gen[i])

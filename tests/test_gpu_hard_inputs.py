@@ -242,7 +242,7 @@ def test_large_batch_launch_structures_match_default(monkeypatch, var, base, mod
     same order (one per CU in the pair geometry), so the gradients, scalars and dP0 are
     bit-identical — B=1024, 4 images per ring-walk workgroup.  BA3C_SCALARS_RIDE: the TfDictOp
     scalar reduction in its own launch after the heads (0) or as one workgroup of conv3's
-    weight-gradient launch (1, default) — the same body, the same scalars."""
+    input-gradient launch (1, default) — the same body, the same scalars."""
     B = 1024
     rs = np.random.RandomState(83)
     state = dev(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8))
@@ -262,8 +262,8 @@ def test_large_batch_launch_structures_match_default(monkeypatch, var, base, mod
         torch.cuda.synchronize()
         out.append((eng.grads.clone(), sc.clone(), dp0))
         if var == "BA3C_SCALARS_RIDE":
-            # the reduction really ran inside conv3's weight-gradient launch (or on its own)
-            assert ("scalars" in eng.kernel_merged("conv3_wgrad")) == (env == "1")
+            # the reduction really ran inside conv3's input-gradient launch (or on its own)
+            assert ("scalars" in eng.kernel_merged("conv3_dgrad")) == (env == "1")
         del eng
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
