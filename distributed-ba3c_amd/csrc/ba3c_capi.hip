@@ -269,12 +269,6 @@ constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
 constexpr int FC_KCHUNK = 160, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;
 static_assert(FC_SPLIT <= FC_SPLIT_MAX, "heads kernel finishes at most FC_SPLIT_MAX chunks");
 static_assert(FC_KCHUNK % GEMM_BK == 0, "k-chunk of whole k-tiles");
-// fc1's forward with its FC_SPLIT chunks summed inside each 64 x 64 workgroup (gemm6_body's
-// chunked K: no partial slabs, one slab for the heads kernel) where those tiles alone fill the
-// chip; the chunks and their order are the split-K launch's, so h is bit-identical either way
-inline bool fc_chunk_acc(const ba3c_handle* h, int B) {
-  return h->g6 && ((B + 63) / 64) * ((h->cfg.fc_neurons + 63) / 64) >= h->cus;
-}
 
 // conv0's weight gradient runs on the main stream while the other weight gradients run on
 // the side stream, so its split-K partials get a region of their own
@@ -664,12 +658,7 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   {
     ProbeScope ps(h, s, BA3C_K_FC1_FWD);
     const dim3 grid((B + 127) / 128, (F + 63) / 64, FC_SPLIT);
-    if (fc_chunk_acc(h, B)) {
-      fc.kchunk = 0;
-      fc.acc_tiles = FC_KCHUNK / GEMM_BK;
-      hipLaunchKernelGGL((gemm6_kernel<64, 64, 2, 2, FcFwd, 4>), dim3((B + 63) / 64, (F + 63) / 64, 1),
-                         dim3(GEMM_THREADS), 0, s, fc);
-    } else if (h->g6 && B <= 64)   // 64-row tiles: same per-row K order, half the dead rows staged
+    if (h->g6 && B <= 64)   // 64-row tiles: same per-row K order, half the dead rows staged
       hipLaunchKernelGGL((gemm6_kernel<64, 64, 2, 2, FcFwd, 4>), dim3((B + 63) / 64, grid.y, grid.z),
                          dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
@@ -836,22 +825,11 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // conv3
   {
     WgradPlan pl = plan_wgrad(576, 64, B * 25, 128, 64);
-    ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
-    ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0,
-                                           h->band ? w.am(AM_DP2, h) : nullptr};
-    // The input gradient splits its k-tiles over two wave groups of a 512-thread workgroup
-    // (KS = 2) at every batch (each image's dP2 rounds the same in any batch, like the
-    // forward); the weight gradient does for B <= OVERLAP_B (r02x: KS = 2 at B=2048 35 -> 45 us),
-    // on every launch path, so the multi-job and separate launches agree bit for bit
-    const dim3 gd((d.M + 63) / 64, (d.N + 63) / 64, 1), gw((pl.M + 127) / 128, (pl.N + 63) / 64, pl.S);
-    if (mj) {
-      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, decltype(d), 4, 2>, Gemm6Job<128, 64, 4, 1, decltype(g), 4, 2>,
-                          NoJob, true>(s, d, gd, g, gw, 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
-      h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_CONV3_WGRAD;
-    } else if (h->band) {
-      // input gradient first: it publishes dY3's per-image maxima, the weight gradient's scale
-      // (both on `s`, whatever the side-stream setting); the deferred TfDictOp reduction rides
-      // on it as one extra workgroup
+    if (h->band) {
+      // whole-image kernels (ba3c_conv3.h) at every batch: an image's dP2 rounds the same in
+      // any batch.  Input gradient first: it publishes dY3's per-image maxima, the weight
+      // gradient's scale (both on `s`, whatever the side-stream setting); the deferred
+      // TfDictOp reduction rides on it as one extra workgroup
       const Conv3Args da{w.dy3, w.wt6 + 2 * (size_t)WT_C3D, w.wexp + WJ_C3D, w.dp2, nullptr,
                          w.am(AM_DP2, h), B, w.am(AM_DY3, h)};
       if (big && h->pend_scalars) {
@@ -870,16 +848,11 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       }
       HIP_TRY(hipGetLastError());
       pl.S = gx;   // one slab per workgroup
-    } else {
-      const bool deep = (int)(gw.x * gw.y * gw.z) < h->cus;   // launch_gemm's ring depth
-      if (big && h->pend_scalars && h->g6 && !deep) {
-        CHECK((launch_multi<false, Gemm6Job<128, 64, 4, 1, decltype(g), 2>, ScalarsJob>(
-            ws, g, gw, h->scalars_args, dim3(1), 0, dim3(0, 1, 1), h, BA3C_K_CONV3_WGRAD)));
-        h->merged[BA3C_K_CONV3_WGRAD] |= 1u << BA3C_K_SCALARS;   // the reduction rode on this launch
-        h->pend_scalars = false;
-      } else if (big) CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
-      else CHECK((launch_gemm<128, 64, 4, 1, decltype(g), 2>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
-      CHECK((launch_gemm<64, 64, 2, 2, decltype(d), 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
+    } else {   // BA3C_GENERIC: the fp32-MFMA GEMM engine
+      ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};
+      ConvDgrad<7, 7, 64, 3, 3, 64, false> d{w.dy3, nullptr, W3c, w.dp2, B * 49, 64, 576, 0, nullptr};
+      CHECK((launch_gemm<128, 64, 4, 1>(h, ws, BA3C_K_CONV3_WGRAD, g, pl.S)));
+      CHECK((launch_gemm<64, 64, 2, 2>(h, s, BA3C_K_CONV3_DGRAD, d, 1)));
     }
     CHECK(conv_reduce(pl, 3, 64, 64, w.part_3));
     CHECK(fork());
@@ -1044,7 +1017,7 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
               bool defer_scalars = false) {
   HeadsArgs a{};
   a.fcpart = w.fcpart;
-  a.fc_split = fc_chunk_acc(h, B) ? 1 : FC_SPLIT;
+  a.fc_split = FC_SPLIT;
   a.per = h->per;
   a.wstride = h->wstride;
   a.fc_w1 = prm + h->tensors[h->idx_fc1].offset;
@@ -1081,13 +1054,7 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
     // features per lane unrolled (heads_sample): the smallest instantiation that covers F
     const int F = a.F;
     const dim3 g((B + 3) / 4), t(256);
-    if (a.fc_split == 1) {   // fc1's chunks already summed (fc_chunk_acc)
-      if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, 1>), g, t, 0, s, a);
-      else if (F <= 128) hipLaunchKernelGGL((heads_kernel<2, 1>), g, t, 0, s, a);
-      else if (F <= 256) hipLaunchKernelGGL((heads_kernel<4, 1>), g, t, 0, s, a);
-      else if (F <= 512) hipLaunchKernelGGL((heads_kernel<8, 1>), g, t, 0, s, a);
-      else hipLaunchKernelGGL((heads_kernel<0, 1>), g, t, 0, s, a);
-    } else if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, FC_SPLIT>), g, t, 0, s, a);
+    if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 128) hipLaunchKernelGGL((heads_kernel<2, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 256) hipLaunchKernelGGL((heads_kernel<4, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 512) hipLaunchKernelGGL((heads_kernel<8, FC_SPLIT>), g, t, 0, s, a);
@@ -1598,8 +1565,7 @@ int ba3c_kernel_split(const ba3c_handle* h, int32_t kid) {
     case BA3C_K_CONV2_DGRAD:
     case BA3C_K_CONV1_WGRAD:
     case BA3C_K_CONV2_WGRAD: return h->band ? 3 : 1;
-    // conv3: whole-image fp16x3 kernels (the backward ones above OVERLAP_B; below it the
-    // multi-job bf16x6 GEMMs)
+    // conv3: whole-image fp16x3 kernels (ba3c_conv3.h)
     case BA3C_K_CONV3_FWD:
     case BA3C_K_CONV3_DGRAD:
     case BA3C_K_CONV3_WGRAD: return h->band ? 3 : (h->g6 ? 6 : 1);

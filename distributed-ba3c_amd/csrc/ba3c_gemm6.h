@@ -21,8 +21,6 @@
 //    rows 4p..4p+3 of the operand; lane i receives operand row i of the 4 K rows) — the
 //    4 K rows of each 32-lane half land in 4 distinct 64-byte bank windows.
 #pragma once
-#include <type_traits>
-#include <utility>
 #include "ba3c_gemm.h"
 #include "ba3c_split.h"
 #include "ba3c_wgrad6.h"   // lds_tr16
@@ -46,15 +44,6 @@ struct Gemm6Lds {
   static constexpr int PB = P::B_KCONTIG ? BN * G6_RP : GEMM_BK * TPB;
   static constexpr int BYTES = 3 * (PA + PB);
 };
-
-// A problem with an `acc_tiles` member may ask for its K to be summed in chunks of acc_tiles
-// k-tiles inside one workgroup: each chunk accumulates from zero and the chunk sums are added
-// in order (tot = c0; tot += c1; ...), exactly the arithmetic of a split-K launch whose slabs
-// are summed in z order afterwards — without the slabs.
-template <class P, class = void>
-struct HasAccTiles : std::false_type {};
-template <class P>
-struct HasAccTiles<P, std::void_t<decltype(std::declval<P>().acc_tiles)>> : std::true_type {};
 
 // (bx, by, bz): the output tile and K chunk (blockIdx of a plain launch; ba3c_multi.h passes
 // its own); lds: KS * Gemm6Lds<BM, BN, P>::BYTES, 16-byte aligned.
@@ -181,28 +170,6 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  // in-workgroup chunked K (HasAccTiles): the running sum of the finished chunks
-  constexpr bool CACC = HasAccTiles<P>::value;
-  static_assert(!CACC || KS == 1, "chunked K runs in one wave group");
-  int acc_tiles = 0;
-  if constexpr (CACC) acc_tiles = p.acc_tiles;
-  f32x16 tot[TM][TN];
-  auto chunk_end = [&](int t) {   // t: the k-tile just accumulated
-    if constexpr (CACC) {
-      if (acc_tiles > 0 && (t + 1) % acc_tiles == 0) {   // uniform
-        const bool first = t + 1 == acc_tiles;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              tot[a][b][r] = first ? acc[a][b][r] : tot[a][b][r] + acc[a][b][r];
-              acc[a][b][r] = 0.f;
-            }
-      }
-    }
-  };
 
   const int li = lane & 31, lh = lane >> 5;
   // fragment base of this lane: row reads at [row li][K 8 lh]; transposed reads: lane 4q + p
@@ -264,7 +231,6 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
       store(st);
       __syncthreads();
       tile(kk + st * BK);
-      chunk_end(it + st);
       __syncthreads();
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -275,16 +241,7 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
       store(st);
       __syncthreads();
       tile(kbeg + (it + st) * BK);
-      chunk_end(it + st);
       __syncthreads();
-    }
-  }
-  if constexpr (CACC) {
-    if (acc_tiles > 0) {
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = tot[a][b];
     }
   }
 

@@ -359,8 +359,6 @@ struct FcFwd {
   int M, N, K, kchunk;
   float* part;          // split-K (kchunk > 0): raw partial slabs [z][M][N]; the heads kernel
                         // (ba3c_small.h) sums them in z order and applies the legacy epilogue
-  int acc_tiles;        // > 0 (with kchunk = 0): the same chunks of acc_tiles k-tiles summed in
-                        // order inside the workgroup (gemm6_body), written as the one slab z = 0
 
   __device__ int a_row(int m) const { return m < M ? m * 1600 : -1; }
   __device__ ARaw a_load(int row, int k, int kend) const {

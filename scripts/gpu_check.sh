@@ -18,3 +18,8 @@ for D in 1 0; do
   echo -n "direct=$D "
   grep -h '^{' gpurun_out/$T/sync_d$D.log | python -c "import sys,json; d=json.loads(sys.stdin.readline()); print(d['ms_per_step'], json.dumps(d['exchange']['timeline']))"
 done
+# optional same-box A/B: scripts/gpu_check.sh TAG KERNEL LIB...
+if [ -n "$2" ]; then
+  k=$2; shift 2
+  bash scripts/gpu_abk.sh $T/ab $k default "$@"
+fi
