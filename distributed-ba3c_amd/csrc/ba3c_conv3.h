@@ -50,6 +50,19 @@ struct Conv3G {
   static constexpr int V4PT = (NV4 + 255) / 256;        // per thread
   static constexpr int WSPLIT = KH * KW * CIN * COUT;   // 16-bit elements between weight planes
   static_assert(PP >= 2 * SPB && PP % 16 == 0 && RP % 16 == 0 && NB == 4, "conv3 layout");
+  // DG: does tap (kh, kw) of m-block j read any non-padding input for a real output pixel?
+  // (m-block 3 holds pixel 48 alone, whose only such tap is (0, 0): its other 16 k-steps
+  // multiply zeros and are not issued — 22 % of the input gradient's MFMAs.  The first MBL
+  // m-blocks use every tap and run in the main k-loop; the rest (DG: m-block 3) run their live
+  // k-steps in a loop of their own — skipping inside the main loop made the compiler spill.)
+  __host__ __device__ static constexpr bool live(int j, int kh, int kw) {
+    for (int r = 16 * j; r < 16 * j + 16 && r < MROWS; ++r) {
+      const int y = r / HO + kh - PAD, x = r % HO + kw - PAD;
+      if (y >= 0 && y < HI && x >= 0 && x < HI) return true;
+    }
+    return false;
+  }
+  static constexpr int MBL = DG ? 3 : MB;
   static_assert(LDS_BYTES <= 64 * 1024, "two workgroups per CU");
 };
 
@@ -145,24 +158,64 @@ __device__ __forceinline__ void conv3_body(const Conv3Args& a, int bx, int gx, c
     f32x4 acc[G::MB];
 #pragma unroll
     for (int j = 0; j < G::MB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the m-blocks past MBL: only their live k-steps
 #pragma unroll
-    for (int t = 0; t < G::NT; ++t) {
+    for (int j = G::MBL; j < G::MB; ++j)
+#pragma unroll
+      for (int t = 0; t < G::NT; ++t) {
+        const int tap = t / G::K32, ch = t - tap * G::K32;
+        const int kh = tap / G::KW, kw = tap - kh * G::KW;
+        if (!G::live(j, kh, kw)) continue;
+        const int toff = kh * G::RP + kw * G::PP + ch * 64;
+        u32x4 av[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * G::SPB);
+          av[s] = u32x4{u.x, u.y, u.z, u.w};
+        }
+#pragma unroll
+        for (int pr = 0; pr < SP::NPROD; ++pr) acc[j] = SP::mfma(av[SP::pa(pr)], bw[t][SP::pb(pr)], acc[j]);
+      }
+    // A fragments double-buffered: k-step t + 1's LDS reads are issued before k-step t's
+    // MFMAs (one set left every k-step waiting a full LDS round trip)
+    auto read_a = [&](int t, u32x4 (&av)[2][G::MB]) {
       const int tap = t / G::K32, ch = t - tap * G::K32;
       const int kh = tap / G::KW, kw = tap - kh * G::KW;
       const int toff = kh * G::RP + kw * G::PP + ch * 64;
-      u32x4 av[2][G::MB];
 #pragma unroll
-      for (int j = 0; j < G::MB; ++j)
+      for (int j = 0; j < G::MBL; ++j)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * G::SPB);
           av[s][j] = u32x4{u.x, u.y, u.z, u.w};
         }
+    };
+    // (the input gradient's four m-blocks leave no registers for a second set: single-buffered)
+    constexpr bool DBUF = !DG;
+    u32x4 avb[DBUF ? 2 : 1][2][G::MB];
+    if constexpr (DBUF) read_a(0, avb[0]);
+#pragma unroll
+    for (int t = 0; t < G::NT; ++t) {
+      if constexpr (DBUF) {
+        if (t + 1 < G::NT) read_a(t + 1, avb[(t + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);   // keep those reads ahead of the MFMAs
+      } else {
+        const int tap = t / G::K32, ch = t - tap * G::K32;
+        const int toff = (tap / G::KW) * G::RP + (tap % G::KW) * G::PP + ch * 64;
+#pragma unroll
+        for (int j = 0; j < G::MBL; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const uint4 u = *reinterpret_cast<const uint4*>(lds + abase[j] + toff + s * G::SPB);
+            avb[0][s][j] = u32x4{u.x, u.y, u.z, u.w};
+          }
+      }
       // a1b1, a1b2, a2b1, interleaved over the m-blocks
 #pragma unroll
       for (int pr = 0; pr < SP::NPROD; ++pr)
 #pragma unroll
-        for (int j = 0; j < G::MB; ++j) acc[j] = SP::mfma(av[SP::pa(pr)][j], bw[t][SP::pb(pr)], acc[j]);
+        for (int j = 0; j < G::MBL; ++j)
+          acc[j] = SP::mfma(avb[DBUF ? (t & 1) : 0][SP::pa(pr)][j], bw[t][SP::pb(pr)], acc[j]);
     }
 
     // epilogue (16x16 C layout: lane holds column li, rows 4 lq + r of each m-block); the
