@@ -22,9 +22,9 @@ SHORT = [  # (regex on the kernel symbol, bench kernel id)
     (r"(conv_band6[rp]?_kernel|multi_kernel_w2)<.*BandGeom<22, 22, 64, 32", "conv2_dgrad"),
     (r"wgrad6?w?_(band_)?kernel<.*Geom<40, 40, 32", "conv1_wgrad"),
     (r"wgrad6?_(band_)?kernel<.*Geom<18, 18, 32", "conv2_wgrad"),
-    (r"ConvFwd<false, 7, 7, 64", "conv3_fwd"),
-    (r"ConvDgrad<7, 7, 64", "conv3_dgrad"),
-    (r"ConvWgrad<false, 7, 7, 64", "conv3_wgrad"),
+    (r"conv3_band_kernel<false>|ConvFwd<false, 7, 7, 64", "conv3_fwd"),
+    (r"conv3_band_kernel<true>|Conv3DJob|ConvDgrad<7, 7, 64", "conv3_dgrad"),
+    (r"conv3_wgrad_kernel|ConvWgrad<false, 7, 7, 64", "conv3_wgrad"),
     (r"FcFwd", "fc1_fwd"), (r"FcDgrad", "fc1_dgrad"),
     (r"gemm6?_kernel<128, 64, 2, 2, ba3c::BatchWgrad", "fc1_wgrad"),
     (r"gemm6?_kernel<128, 32, 4, 1, ba3c::BatchWgrad", "head_wgrad"),
