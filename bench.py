@@ -326,7 +326,7 @@ def exchange_report(tr, batch, timeline, iters, world):
     return {"buckets": {"fc1_heads": {"bytes": 4 * (total - off)}, "conv": {"bytes": 4 * off}},
             "backend": dist.get_backend() if dist.is_initialized() else None,
             # bucket sums through RCCL driven directly (rccl.py) or torch's collective
-            "collective": "rccl-direct" if getattr(opt, "_rccl", None) is not None else "torch",
+            "collective": "rccl-direct" if getattr(opt, "_rccl", None) else "torch",
             "timeline": tl,
             "phase2_launch_ms": {k: {"with_exchange": round(a, 4), "exchange_off": round(b, 4)}
                                  for k, a, b in zip(PHASE2_KERNELS, el[len(names):len(names) + n],

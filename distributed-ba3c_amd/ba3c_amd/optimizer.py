@@ -7,6 +7,7 @@ in (single replica).  SyncReplicasOptimizer replaces the parameter-server accumu
 an RCCL all-reduce of the flat clipped-gradient buffer (torch.distributed 'nccl' == RCCL).
 """
 import os
+import sys
 import time
 
 import numpy as np
@@ -367,11 +368,18 @@ class SyncReplicasOptimizer(object):
         flag = os.environ.get("BA3C_DIRECT_RCCL", "1")
         if flag not in ("0", "1"):
             raise ValueError("BA3C_DIRECT_RCCL must be 0 or 1 (got %r)" % flag)
-        if flag == "0" or dist.get_backend(self.group) != "nccl":
+        if flag == "0" or dist.get_backend(self.group) != "nccl" or self._rccl is False:
             return None
         if self._rccl is None:
-            from .rccl import RcclComm
-            self._rccl = RcclComm(self.group, device)
+            from .rccl import RcclComm, RcclError
+            try:
+                self._rccl = RcclComm(self.group, device)
+            except (OSError, AttributeError, RcclError) as e:
+                # the library or the communicator is unavailable: torch's collective does the
+                # same sums (every rank raises alike, ncclCommInitRank being collective)
+                print("ba3c: direct RCCL unavailable (%s); using torch's collective" % e, file=sys.stderr)
+                self._rccl = False
+                return None
         return self._rccl
 
     def aggregate_bucket_async(self, engine, t0, t1, off0, off1, marks=None, last=False):

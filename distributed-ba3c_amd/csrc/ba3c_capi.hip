@@ -266,7 +266,10 @@ WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN) {
 constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
 // FC1 fwd split-K: 10 fixed chunks of 5 k-tiles (batch-independent rounding).  r02: 416 (4
 // chunks of 13 k-tiles) left B=32 with 8 workgroups walking 13 dependent k-tiles (17.6 us)
-constexpr int FC_KCHUNK = 160, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;
+#ifndef BA3C_FC_KCHUNK
+#define BA3C_FC_KCHUNK 160
+#endif
+constexpr int FC_KCHUNK = BA3C_FC_KCHUNK, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;
 static_assert(FC_SPLIT <= FC_SPLIT_MAX, "heads kernel finishes at most FC_SPLIT_MAX chunks");
 static_assert(FC_KCHUNK % GEMM_BK == 0, "k-chunk of whole k-tiles");
 

@@ -171,8 +171,8 @@ def test_sync_replicas_rccl_allreduce_world1_equals_single_replica_step(monkeypa
                             world_size=1, device_id=torch.device("cuda", torch.cuda.current_device()))
     try:
         got = run(True)
-        assert (opts[0]._rccl is not None) == (direct == "1")
-        if opts[0]._rccl is not None:
+        assert bool(opts[0]._rccl) == (direct == "1")
+        if opts[0]._rccl:
             opts[0]._rccl.close()
     finally:
         dist.destroy_process_group()
