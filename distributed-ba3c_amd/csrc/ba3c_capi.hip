@@ -1057,7 +1057,10 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
     // features per lane unrolled (heads_sample): the smallest instantiation that covers F
     const int F = a.F;
     const dim3 g((B + 3) / 4), t(256);
-    if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, FC_SPLIT>), g, t, 0, s, a);
+    // the reference's Atari action sets are mostly 4 actions: compile-time A there (heads_sample)
+    if (a.A == 4 && F <= 128 && F > 64) hipLaunchKernelGGL((heads_kernel<2, FC_SPLIT, 4>), g, t, 0, s, a);
+    else if (a.A == 4 && F <= 512 && F > 256) hipLaunchKernelGGL((heads_kernel<8, FC_SPLIT, 4>), g, t, 0, s, a);
+    else if (F <= 64) hipLaunchKernelGGL((heads_kernel<1, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 128) hipLaunchKernelGGL((heads_kernel<2, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 256) hipLaunchKernelGGL((heads_kernel<4, FC_SPLIT>), g, t, 0, s, a);
     else if (F <= 512) hipLaunchKernelGGL((heads_kernel<8, FC_SPLIT>), g, t, 0, s, a);

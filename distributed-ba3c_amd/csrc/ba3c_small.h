@@ -77,12 +77,18 @@ __device__ __forceinline__ double wave_max_d(double v, int w = 64) { return wave
 // first sum — one global round trip per sample instead of one per 64 features (F=512: eight
 // dependent HBM round trips per wave were most of the B=2048 heads launch).  The sums, their z
 // order and every product are unchanged.  FCH == 0: the runtime loop over f (any F).
-template <int FCH, int NZ>
+// AT > 0: the action count as a compile-time constant (AT == p.A).  With the runtime count the
+// head-weight loads sat in `a < A` branches, each followed by a wait for every outstanding load:
+// ~80 dependent global round trips per sample (r04 ISA) — the heads launch's whole time.  With
+// AT every weight load of a lane's features is unconditional (features past F read feature
+// F - 1 and are multiplied by zero), so they are all in flight together.
+template <int FCH, int NZ, int AT>
 __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane) {
-  const int A = p.A;
-  double acc[MAXA];
+  const int A = AT ? AT : p.A;
+  constexpr int NA = AT ? AT : MAXA;                 // loop bound over actions
+  double acc[NA];
 #pragma unroll
-  for (int a = 0; a < MAXA; ++a) acc[a] = 0.0;
+  for (int a = 0; a < NA; ++a) acc[a] = 0.0;
   double accv = 0.0;
   float* hn = p.h + (size_t)n * p.F;
   unsigned long long pos = 0;
@@ -121,13 +127,14 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
 #pragma unroll
     for (int i = 0; i < FCH; ++i) {
       const int f = lane + 64 * i;
-      if (f < p.F) {
+      if (AT || f < p.F) {            // AT: hv32 is 0 past F, the clamped loads are harmless
+        const int fc = AT ? min(f, p.F - 1) : f;
         const double hv = hv32[i];
-        const float* wr = p.piW + (size_t)f * A;
+        const float* wr = p.piW + (size_t)fc * A;
 #pragma unroll
-        for (int a = 0; a < MAXA; ++a)
-          if (a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
-        accv = fma(hv, (double)p.vW[f], accv);
+        for (int a = 0; a < NA; ++a)
+          if (AT || a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
+        accv = fma(hv, (double)p.vW[fc], accv);
       }
     }
   }
@@ -154,15 +161,15 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
     const double hv = h32;
     const float* wr = p.piW + (size_t)f * A;
 #pragma unroll
-    for (int a = 0; a < MAXA; ++a)
-      if (a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
+    for (int a = 0; a < NA; ++a)
+      if (AT || a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
     accv = fma(hv, (double)p.vW[f], accv);
   }
   const bool mine = lane < A;
   double z = 0.0;                                   // z[lane] for lane < A
 #pragma unroll
-  for (int a = 0; a < MAXA; ++a) {
-    if (a < A) {
+  for (int a = 0; a < NA; ++a) {
+    if (AT || a < A) {
       const double za = wave_sum_d(acc[a]) + (double)p.pib[a];
       if (lane == a) z = za;
     }
@@ -199,11 +206,11 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
   const double dV = (V - Rn) * invB;
   // [dz | dV | 0...] row for the head weight-gradient product
   if (lane < MAXA) p.dzv[(size_t)n * MAXA + lane] = (float)(lane == A ? dV : dz);
-  double dza[MAXA];
+  double dza[NA];
 #pragma unroll
-  for (int a = 0; a < MAXA; ++a) {
+  for (int a = 0; a < NA; ++a) {
     dza[a] = 0.0;
-    if (a < A) {                                     // uniform branch: A broadcasts only
+    if (AT || a < A) {                               // uniform branch: A broadcasts only
       const unsigned long long u = __double_as_longlong(dz);
       const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, a), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), a);
       dza[a] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
@@ -214,12 +221,31 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
     const float* wr = p.piW + (size_t)f * A;
     double g = dV * (double)p.vW[f];
 #pragma unroll
-    for (int a = 0; a < MAXA; ++a)
-      if (a < A) g = fma(dza[a], (double)wr[a], g);
+    for (int a = 0; a < NA; ++a)
+      if (AT || a < A) g = fma(dza[a], (double)wr[a], g);
     if (p.legacy && !(hn[f] > 0.f)) g = 0.0;
     dhn[f] = (float)g;
   };
-  if constexpr (FCH > 0) {
+  if constexpr (FCH > 0 && AT > 0) {
+    // every feature's weight loads first (clamped, unconditional), then the stores
+    double g[FCH];
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int fc = min(lane + 64 * i, p.F - 1);
+      const float* wr = p.piW + (size_t)fc * A;
+      g[i] = dV * (double)p.vW[fc];
+#pragma unroll
+      for (int a = 0; a < AT; ++a) g[i] = fma(dza[a], (double)wr[a], g[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int f = lane + 64 * i;
+      if (f < p.F) {
+        if (p.legacy && !(hn[f] > 0.f)) g[i] = 0.0;
+        dhn[f] = (float)g[i];
+      }
+    }
+  } else if constexpr (FCH > 0) {
 #pragma unroll
     for (int i = 0; i < FCH; ++i)
       if (lane + 64 * i < p.F) dh_one(lane + 64 * i);
@@ -255,9 +281,11 @@ __device__ __forceinline__ void scalars_block(const float* terms, int B, float b
     float v[U][6];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float* tn = terms + (size_t)(n0 + 256 * u) * NTERMS;
+      // unconditional loads (past B: sample B - 1 again, not added): a conditional load was a
+      // branch and a wait per value, 48 dependent round trips at B = 32
+      const float* tn = terms + (size_t)min(n0 + 256 * u, B - 1) * NTERMS;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) v[u][k] = n0 + 256 * u < B ? ld_agent(tn + k) : 0.f;
+      for (int k = 0; k < 6; ++k) v[u][k] = ld_agent(tn + k);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -269,8 +297,14 @@ __device__ __forceinline__ void scalars_block(const float* terms, int B, float b
     }
   }
   unsigned long long rc = 0;
-  if (relu_count)
-    for (int i = t; i < RELU_SLOTS; i += 256) rc += ld_agent(relu_count + i);
+  if (relu_count) {
+    static_assert(RELU_SLOTS % 256 == 0, "whole slots per thread");
+    unsigned long long r[RELU_SLOTS / 256];           // all in flight, then the (exact) sum
+#pragma unroll
+    for (int j = 0; j < RELU_SLOTS / 256; ++j) r[j] = ld_agent(relu_count + t + 256 * j);
+#pragma unroll
+    for (int j = 0; j < RELU_SLOTS / 256; ++j) rc += r[j];
+  }
 #pragma unroll
   for (int i = 0; i < 5; ++i) s[i] = wave_sum_d(s[i]);
   mx = wave_max_d(mx);
@@ -316,11 +350,11 @@ __global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B,
 // (s_waitcnt 0) and the workgroup barriers BEFORE thread 0 increments the counter; the last
 // workgroup reads the words only with agent-scope loads (ld_agent: global_load sc1) after its
 // barrier.  The counter itself is a device atomic.  No step relies on release/acquire ordering.
-template <int FCH, int NZ>
+template <int FCH, int NZ, int AT = 0>
 __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n < p.B) heads_sample<FCH, NZ>(p, n, lane);
+  if (n < p.B) heads_sample<FCH, NZ, AT>(p, n, lane);
   if (p.train && p.scalars) {                 // uniform over the grid
     // terms go out with st_agent and ReLU counts with device atomics; each wave waits for its
     // own stores before the workgroup's arrival is counted (no L2 write-back fence)
