@@ -666,8 +666,11 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
                          dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, 4>), grid, dim3(GEMM_THREADS), 0, s, fc);
+#ifndef BA3C_FC_DEPTH
+#define BA3C_FC_DEPTH 2       // k-tile ring depth of fc1's forward at full grids (A/B)
+#endif
     else if (h->g6)
-      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);
+      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, BA3C_FC_DEPTH>), grid, dim3(GEMM_THREADS), 0, s, fc);
     else
       hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);
   }
@@ -777,9 +780,12 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     if (mj_fc && !big)
       CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, 4>, Gemm6Job<128, 32, 4, 1, BatchWgrad, 4>,
                           Gemm6Job<128, 64, 2, 2, BatchWgrad, 4>>(s, d, gd, g, gh, gf, gff, h, BA3C_K_FC1_DGRAD)));
+#ifndef BA3C_FCD_DEPTH
+#define BA3C_FCD_DEPTH 2      // k-tile ring depth of the large-batch fc1 backward jobs (A/B)
+#endif
     else if (mj_fc)
-      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, 2>, Gemm6Job<128, 32, 4, 1, BatchWgrad, 2>,
-                          Gemm6Job<128, 64, 2, 2, BatchWgrad, 2>>(s, d, gd, g, gh, gf, gff, h, BA3C_K_FC1_DGRAD)));
+      CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, BA3C_FCD_DEPTH>, Gemm6Job<128, 32, 4, 1, BatchWgrad, BA3C_FCD_DEPTH>,
+                          Gemm6Job<128, 64, 2, 2, BatchWgrad, BA3C_FCD_DEPTH>>(s, d, gd, g, gh, gf, gff, h, BA3C_K_FC1_DGRAD)));
     else
       CHECK((launch_gemm<128, 32, 4, 1>(h, ws, BA3C_K_HEAD_WGRAD, g, pl.S)));
     ReduceMap mp{};
