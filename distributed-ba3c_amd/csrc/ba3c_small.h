@@ -693,27 +693,30 @@ __global__ void __launch_bounds__(256) update_kernel(const UpdateArgs a, const T
   const int beg = c * UPD_CHUNK;
   const int end = min(tt.numel[t], beg + UPD_CHUNK);
   const long long o = tt.off[t];
-  const float f = a.clip_part ? clip_factor(tt, t, a.clip_part) : 0.f;
-  const float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1])
-                                                 : a.alpha;
   // all loads of the thread's UPD_CHUNK / 256 elements are issued before any store: the
   // stores to p / s0 / s1 may alias later loads as far as the compiler knows, which would
   // otherwise serialise one HBM round trip per element.  Per-element arithmetic unchanged.
   constexpr int PER = UPD_CHUNK / 256;
   constexpr bool S0 = OPT != 1, S1 = OPT == 0 || OPT == 3 || OPT == 5;
   float gv[PER], pv[PER], s0v[PER], s1v[PER];
+  // unconditional loads (past the chunk's end: its last element again, zeroed below): a load
+  // in an `i < end` branch let only one element's loads be in flight at a time (r04 ISA)
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = beg + threadIdx.x + 256 * j;
-    gv[j] = pv[j] = s0v[j] = s1v[j] = 0.f;
-    if (i < end) {
-      const long long k = o + i;
-      gv[j] = a.g[k];
-      pv[j] = a.p[k];
-      if constexpr (S0) s0v[j] = a.s0[k];
-      if constexpr (S1) s1v[j] = a.s1[k];
-    }
+    const long long k = o + min(i, end - 1);
+    gv[j] = a.g[k];
+    pv[j] = a.p[k];
+    s0v[j] = S0 ? a.s0[k] : 0.f;
+    s1v[j] = S1 ? a.s1[k] : 0.f;
   }
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (beg + (int)threadIdx.x + 256 * j >= end) gv[j] = pv[j] = s0v[j] = s1v[j] = 0.f;
+  // the clip factor and Adam's powers after the element loads (their latency overlaps)
+  const float f = a.clip_part ? clip_factor(tt, t, a.clip_part) : 0.f;
+  const float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1])
+                                                 : a.alpha;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = beg + threadIdx.x + 256 * j;
@@ -790,18 +793,20 @@ __global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, co
   constexpr int PER = UPD_CHUNK / 256;
   constexpr bool S0 = OPT != 1, S1 = OPT == 0 || OPT == 3 || OPT == 5;
   float gv[PER], pv[PER], s0v[PER], s1v[PER];
+  // unconditional loads (past the chunk's end: its last element again, zeroed below): a load
+  // in an `i < end` branch let only one element's loads be in flight at a time (r04 ISA)
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = beg + threadIdx.x + 256 * j;
-    gv[j] = pv[j] = s0v[j] = s1v[j] = 0.f;
-    if (i < end) {
-      const long long k = o + i;
-      gv[j] = a.g[k];
-      pv[j] = a.p[k];
-      if constexpr (S0) s0v[j] = a.s0[k];
-      if constexpr (S1) s1v[j] = a.s1[k];
-    }
+    const long long k = o + min(i, end - 1);
+    gv[j] = a.g[k];
+    pv[j] = a.p[k];
+    s0v[j] = S0 ? a.s0[k] : 0.f;
+    s1v[j] = S1 ? a.s1[k] : 0.f;
   }
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (beg + (int)threadIdx.x + 256 * j >= end) gv[j] = pv[j] = s0v[j] = s1v[j] = 0.f;
   float alpha = (OPT == 0 && a.dev_powers) ? adam_alpha(a.lr, a.dev_powers[0], a.dev_powers[1]) : a.alpha;
   asm volatile("" : "+v"(alpha) : : "memory");   // the powers are read before this chunk publishes
   // phase 1: the chunk's sum of squares, in sumsq_kernel's order (i = beg + tid + 256 j)
@@ -866,7 +871,8 @@ __global__ void __launch_bounds__(256) clip_range_kernel(float* __restrict__ g, 
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = beg + threadIdx.x + 256 * j;
-    gv[j] = i < end ? gt[i] : 0.f;
+    const float v = gt[min(i, end - 1)];        // unconditional: every load in flight at once
+    gv[j] = i < end ? v : 0.f;
   }
   float ss = 0.f;
 #pragma unroll
