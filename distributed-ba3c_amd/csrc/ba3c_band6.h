@@ -131,20 +131,24 @@ struct Band6Ops {
                                float4& v, uint32_t& cd) {
     const unsigned nvec = (unsigned)(rows_out + G::KH - 1) * G::WS * Q;
     const unsigned pix = f / Q, cq = f - pix * Q;
-    v = f4zero();
-    cd = 0;
     if constexpr (G::SRC == 0) {
+      // (the forward layouts keep the branch: branch-free measured 0.289 -> 0.297 ms for conv1's
+      // ring walk, 0.093 -> 0.094 ms for conv2)
+      v = f4zero();
+      cd = 0;
       const float* srcb = a.src + ((size_t)(img * G::HS + y0) * G::WS) * G::CIN + cb;
       if (f < nvec) v = *reinterpret_cast<const float4*>(srcb + pix * G::CIN + cq * 4);
     } else {
+      // branch-free loads (ld4 / ld_u8x4 read zeros for a rejected element): a load in a
+      // branch made the compiler wait for every outstanding load at the join
       const unsigned ry = pix / G::WS, x = pix - ry * G::WS;
       const int uy = (int)(y0 + ry) - G::PADY, ux = (int)x - G::PADX;
-      if (f < nvec && (unsigned)uy < (unsigned)G::UHO && (unsigned)ux < (unsigned)G::UWO) {
-        const size_t ib = (size_t)img * (G::UPH * G::UPW) * G::CIN + cb;
-        const unsigned off = ((uy >> 1) * G::UPW + (ux >> 1)) * G::CIN + cq * 4;
-        v = *reinterpret_cast<const float4*>(a.src + ib + off);
-        cd = *reinterpret_cast<const uint32_t*>(a.code + ib + off);
-      }
+      const bool ok = f < nvec && (unsigned)uy < (unsigned)G::UHO && (unsigned)ux < (unsigned)G::UWO;
+      const size_t e = ok ? (size_t)img * (G::UPH * G::UPW) * G::CIN + cb +
+                                ((uy >> 1) * G::UPW + (ux >> 1)) * G::CIN + cq * 4
+                          : 0;
+      v = ld4(a.src + e, ok);
+      cd = ld_u8x4(a.code + e, ok);
     }
   }
   __device__ static void store1(char* lds, int y0, int rows_out, unsigned f, const float4& v, uint32_t cd,
@@ -201,14 +205,11 @@ struct Band6Ops {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int f = t + 256 * i;
-      v[i] = f4zero();
-      c[i] = 0;
-      if (f < NPI) {
-        const int cq = f % Q, rest = f / Q;
-        const size_t off = ((size_t)img * (G::UPH * G::UPW) + rest) * G::CIN + ph * L::KPH + cq * 4;
-        v[i] = *reinterpret_cast<const float4*>(a.src + off);
-        c[i] = *reinterpret_cast<const uint32_t*>(a.code + off);
-      }
+      const bool ok = f < NPI;                           // branch-free (see load1)
+      const int cq = f % Q, rest = f / Q;
+      const size_t off = ok ? ((size_t)img * (G::UPH * G::UPW) + rest) * G::CIN + ph * L::KPH + cq * 4 : 0;
+      v[i] = ld4(a.src + off, ok);
+      c[i] = ld_u8x4(a.code + off, ok);
     }
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -368,6 +369,14 @@ struct Band6Ops {
             if (t + 1 < L::NT) read_a(t + 1, avb[(t + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);                // keep those reads ahead of the MFMAs
           } else {
+#ifndef BA3C_B6_RINGFENCE
+#define BA3C_B6_RINGFENCE 1   // 0: A/B build without the fence below
+#endif
+            // the weight-ring loads of k-step t + LA stay here: the scheduler otherwise sank them
+            // next to their use, leaving one k-step of lookahead (a vmcnt(0) per k-step, r04 ISA).
+            // Input-gradient layouts only: conv2's whole-map input gradient + weight gradient
+            // 0.265 -> 0.221 ms with the branch-free staging; conv2's forward 0.093 -> 0.095 ms
+            if (BA3C_B6_RINGFENCE && !G::POOL) __builtin_amdgcn_sched_barrier(0);
             read_a(t, avb[0]);
           }
           u32x4 b[L::NS];

@@ -138,23 +138,20 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
       const int pix = f / XQ, cq = f - pix * XQ;
       const int ry = xr0 + pix / G::WS, x = pix - (pix / G::WS) * G::WS;
       const int y = y0 + ry;
-      xv[i] = f4zero();
-      if (f < xn && y < G::HS)
-        xv[i] = *reinterpret_cast<const float4*>(a.x + ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + c0 + cq * 4);
+      // branch-free (ld4 reads zeros for a rejected element): a load in a branch made the
+      // compiler wait for every outstanding load at the join, serialising the prefetch
+      const bool ok = f < xn && y < G::HS;
+      xv[i] = ld4(a.x + (ok ? ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + c0 + cq * 4 : 0), ok);
     }
 #pragma unroll
     for (int i = 0; i < YPT; ++i) {
       const int f = tid + 256 * i;
       const int p = f / YQ, oq = f - p * YQ;
       const int ry = p / G::WO, x = p - ry * G::WO;
-      yv[i] = f4zero();
-      yc[i] = 0;
-      if (f < YN && ry < rows_out) {
-        const int y = y0 + ry;
-        const size_t pidx = (size_t)(img * G::PH + (y >> 1)) * G::PW + (x >> 1);
-        yv[i] = *reinterpret_cast<const float4*>(a.dp + pidx * G::COUT + o0 + oq * 4);
-        yc[i] = *reinterpret_cast<const uint32_t*>(a.code + pidx * G::COUT + o0 + oq * 4);
-      }
+      const bool ok = f < YN && ry < rows_out;
+      const size_t e = ok ? ((size_t)(img * G::PH + ((y0 + ry) >> 1)) * G::PW + (x >> 1)) * G::COUT + o0 + oq * 4 : 0;
+      yv[i] = ld4(a.dp + e, ok);
+      yc[i] = ld_u8x4(a.code + e, ok);
     }
   };
   auto store_band = [&](int band) {
@@ -401,13 +398,10 @@ __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, c
         const int f = tid + 256 * i;
         const int oq = f % YQ, rest = f / YQ;
         const int pc = rest % G::PW, py = (y0 >> 1) + rest / G::PW;
-        yv[i] = f4zero();
-        yc[i] = 0;
-        if (f < YN) {
-          const size_t off = ((size_t)(img * G::PH + py) * G::PW + pc) * G::COUT + oq * 4;
-          yv[i] = *reinterpret_cast<const float4*>(a.dp + off);
-          yc[i] = *reinterpret_cast<const uint32_t*>(a.code + off);
-        }
+        const bool ok = f < YN;                         // branch-free (see wgrad6_body)
+        const size_t off = ok ? ((size_t)(img * G::PH + py) * G::PW + pc) * G::COUT + oq * 4 : 0;
+        yv[i] = ld4(a.dp + off, ok);
+        yc[i] = ld_u8x4(a.code + off, ok);
       }
       return;
     }
