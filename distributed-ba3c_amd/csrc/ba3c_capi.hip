@@ -175,7 +175,7 @@ using GConv2DS = BandGeom<22, 22, 64, 32, 5, 5, 3, false, 1, 8, 4, 4, 7, 7, 14, 
 // split-kernel layouts (scaled fp16 hi/lo planes)
 struct Lay {
   using C1F = Band6<GConv1F, 160, 128, 7, 0, 2, true>;
-  using C2F = Band6<GConv2F, 160, 64, 7, 0, 2>;
+  using C2F = Band6<GConv2F, 160, 64, 7, 0, 2>;   // (double-buffered: 256 VGPRs, neutral, r04)
 #ifndef BA3C_C1D_TILE4
 #define BA3C_C1D_TILE4 1
 #endif

@@ -297,8 +297,11 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int e = tid + 256 * i;                 // entry e = row r * 84 + x: pixel index e
-      ev[i][0] = e < NV ? src[e] : 0u;
-      ev[i][1] = e < NV ? src[e + 2 * G::WS] : 0u;
+      // branch-free (past the band: entry 0 again, stored nowhere): the conditional loads made
+      // the compiler wait for this prefetch before the band's first MFMA (r04 ISA)
+      const int ec = e < NV ? e : 0;
+      ev[i][0] = src[ec];
+      ev[i][1] = src[ec + 2 * G::WS];
     }
   };
   auto store_band = [&]() {
@@ -329,6 +332,14 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
         const uint4 u = a.wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane];
         wf[sp][nt][s] = u32x4{u.x, u.y, u.z, u.w};
       }
+  // the weights are complete before the band loop: otherwise the loop's merged wait state
+  // made every band's first MFMA wait for all loads, the next band's prefetch included
+#pragma unroll
+  for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int s = 0; s < G::KSTEPS; ++s) asm volatile("" : "+v"(wf[sp][nt][s]));
   // this lane's row (window li>>2, sub li&3) of m-block 0 of the wave, per (kstep, tap half)
   const int wi = li >> 2, sub = li & 3;
   constexpr int RP = C0E_PITCH;                     // entry index pitch
@@ -574,8 +585,8 @@ __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, i
       }
       yc[i] = c;
     }
-    xv = tid < G::NXV ? reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C)[tid]
-                      : make_uint4(0, 0, 0, 0);
+    // branch-free (threads past the rows re-read entry 0 and store nothing)
+    xv = reinterpret_cast<const uint4*>(a.x + ((size_t)img * G::HS + y0) * G::WS * G::C)[tid < G::NXV ? tid : 0];
   };
   auto store_band = [&]() {
 #pragma unroll
