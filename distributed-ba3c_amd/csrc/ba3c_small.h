@@ -93,11 +93,69 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
   float* hn = p.h + (size_t)n * p.F;
   unsigned long long pos = 0;
   const size_t MN = (size_t)p.B * p.F;
-  if constexpr (FCH > 0) {
-    float hv32[FCH];
-    if (p.fcpart) {
+  // PRE (FCH > 0 and AT > 0): every value the sample reads besides fc1's partials — the head
+  // weights of the lane's features, the biases, the legacy FC bias, R and the action — is
+  // loaded together with the partials, before the first store.  The stores to h / probs / dzv
+  // may alias those arrays for the compiler, which kept each later group of loads behind the
+  // stores before it: three dependent global round trips per sample, one here.  Same values,
+  // same arithmetic.
+  constexpr bool PRE = FCH > 0 && AT > 0;
+  float wpre[PRE ? FCH : 1][PRE ? AT + 1 : 1];   // [i][a < AT]: pi weights, [i][AT]: v weight
+  float bpre[PRE ? AT + 1 : 1];                  // pi biases, v bias
+  float blg[PRE ? FCH : 1];                      // legacy FC bias of the lane's features
+  float Rpre = 0.f;
+  int apre = 0;
+  float hv32[FCH > 0 ? FCH : 1];
+  if constexpr (PRE) {
+    float pz[FCH][NZ];
+    const int per = p.legacy ? p.per : 1;
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
       // unconditional loads (a feature past F re-reads feature F - 1 and is discarded): a
       // branch around each load made the compiler drain the loads at every join
+      const int f = min(lane + 64 * i, p.F - 1);
+      const size_t e = (size_t)n * p.F + f;
+      // no partials: every z re-reads h (only z = 0 is used) — a pointer select, not a branch
+      const float* src = p.fcpart ? p.fcpart + e : hn + f;
+      const size_t zs = p.fcpart ? MN : 0;
+#pragma unroll
+      for (int z = 0; z < NZ; ++z) pz[i][z] = src[z * zs];
+      const int sidx = f / per;
+      blg[i] = *(p.legacy ? p.fc_w1 + sidx * p.wstride + 1600 * per + (f - sidx * per) : p.pib);
+#pragma unroll
+      for (int a = 0; a < AT; ++a) wpre[i][a] = p.piW[(size_t)f * AT + a];
+      wpre[i][AT] = p.vW[f];
+    }
+#pragma unroll
+    for (int a = 0; a < AT; ++a) bpre[a] = p.pib[a];
+    bpre[AT] = p.vb[0];
+    Rpre = *(p.train ? p.R + n : p.pib);
+    // the action's low word (actions are small and non-negative)
+    apre = *(p.train ? reinterpret_cast<const int*>(p.action + n) : reinterpret_cast<const int*>(p.pib));
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int f = lane + 64 * i;
+      float h32 = pz[i][0];
+      if (p.fcpart) {
+#pragma unroll
+        for (int z = 1; z < NZ; ++z) h32 += pz[i][z];
+        if (p.legacy && f < p.F) {
+          h32 = fmaxf(h32 + blg[i], 0.f);
+          pos += h32 > 0.f;
+        }
+        if (f < p.F) hn[f] = h32;
+      }
+      hv32[i] = f < p.F ? h32 : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const double hv = hv32[i];                      // 0 past F
+#pragma unroll
+      for (int a = 0; a < AT; ++a) acc[a] = fma(hv, (double)wpre[i][a], acc[a]);
+      accv = fma(hv, (double)wpre[i][AT], accv);
+    }
+  } else if constexpr (FCH > 0) {
+    if (p.fcpart) {
       float pz[FCH][NZ];
 #pragma unroll
       for (int i = 0; i < FCH; ++i) {
@@ -127,14 +185,13 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
 #pragma unroll
     for (int i = 0; i < FCH; ++i) {
       const int f = lane + 64 * i;
-      if (AT || f < p.F) {            // AT: hv32 is 0 past F, the clamped loads are harmless
-        const int fc = AT ? min(f, p.F - 1) : f;
+      if (f < p.F) {
         const double hv = hv32[i];
-        const float* wr = p.piW + (size_t)fc * A;
+        const float* wr = p.piW + (size_t)f * A;
 #pragma unroll
         for (int a = 0; a < NA; ++a)
-          if (AT || a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
-        accv = fma(hv, (double)p.vW[fc], accv);
+          if (a < A) acc[a] = fma(hv, (double)wr[a], acc[a]);
+        accv = fma(hv, (double)p.vW[f], accv);
       }
     }
   }
@@ -170,12 +227,12 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
 #pragma unroll
   for (int a = 0; a < NA; ++a) {
     if (AT || a < A) {
-      const double za = wave_sum_d(acc[a]) + (double)p.pib[a];
+      const double za = wave_sum_d(acc[a]) + (double)(PRE ? bpre[a] : p.pib[a]);
       if (lane == a) z = za;
     }
   }
   if (p.fcpart && p.legacy && p.relu_count) relu_count_add(p.relu_count, pos, lane);
-  const double V = wave_sum_d(accv) + (double)p.vb[0];
+  const double V = wave_sum_d(accv) + (double)(PRE ? bpre[PRE ? AT : 0] : p.vb[0]);
   // softmax(z)  (tf.nn.softmax: exp(z - max) / sum)
   const double zmax = wave_max_d(mine ? z : -INFINITY, A);
   const double e = mine ? exp(z - zmax) : 0.0;
@@ -192,8 +249,8 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
   if (p.value && lane == 0) p.value[n] = (float)V;
   if (!p.train) return;
 
-  const double Rn = p.R[n];
-  const int act = (int)p.action[n];
+  const double Rn = PRE ? (double)Rpre : (double)p.R[n];
+  const int act = (int)(PRE ? apre : p.action[n]);
   const double adv = V - Rn;
   const double beta = (double)p.beta, invB = 1.0 / (double)p.B;
   const double pe = pr + 1e-6;
@@ -226,23 +283,17 @@ __device__ __forceinline__ void heads_sample(const HeadsArgs& p, int n, int lane
     if (p.legacy && !(hn[f] > 0.f)) g = 0.0;
     dhn[f] = (float)g;
   };
-  if constexpr (FCH > 0 && AT > 0) {
-    // every feature's weight loads first (clamped, unconditional), then the stores
-    double g[FCH];
-#pragma unroll
-    for (int i = 0; i < FCH; ++i) {
-      const int fc = min(lane + 64 * i, p.F - 1);
-      const float* wr = p.piW + (size_t)fc * A;
-      g[i] = dV * (double)p.vW[fc];
-#pragma unroll
-      for (int a = 0; a < AT; ++a) g[i] = fma(dza[a], (double)wr[a], g[i]);
-    }
+  if constexpr (PRE) {
+    // the preloaded weights; the legacy ReLU mask from the h values this lane stored
 #pragma unroll
     for (int i = 0; i < FCH; ++i) {
       const int f = lane + 64 * i;
+      double g = dV * (double)wpre[i][AT];
+#pragma unroll
+      for (int a = 0; a < AT; ++a) g = fma(dza[a], (double)wpre[i][a], g);
       if (f < p.F) {
-        if (p.legacy && !(hn[f] > 0.f)) g[i] = 0.0;
-        dhn[f] = (float)g[i];
+        if (p.legacy && !(hv32[i] > 0.f)) g = 0.0;
+        dhn[f] = (float)g;
       }
     }
   } else if constexpr (FCH > 0) {
