@@ -557,7 +557,10 @@ int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, con
   const Conv0SArgs sa{state, reinterpret_cast<const uint4*>(w.wt + WT_C0S), w.p0, train ? w.c0 : nullptr,
                       train ? w.relu : nullptr, B, w.wexp + WX_CONV0, w.am(AM_P0, h)};
   ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
-  return launch_multi<false, Conv0SJob, WPrep6Job>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)), rest,
+  // two workgroups per CU (the register budget of conv0's plain kernel): without the bound the
+  // compiler gave the fused body 216 VGPRs + 52 AGPRs, one wave per SIMD, so at B=32 the 160 conv0
+  // and 192 weight-prep workgroups did not fit the 256 CUs in one round
+  return launch_multi<true, Conv0SJob, WPrep6Job>(s, sa, dim3(std::min(FW_P0S, B * Conv0S::NBANDS)), rest,
                                                   dim3(64, rest.jobs.njobs));
 }
 
