@@ -844,21 +844,34 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       // TfDictOp reduction rides on it as one extra workgroup
       const Conv3Args da{w.dy3, w.wt6 + 2 * (size_t)WT_C3D, w.wexp + WJ_C3D, w.dp2, nullptr,
                          w.am(AM_DP2, h), B, w.am(AM_DY3, h)};
-      if (big && h->pend_scalars) {
-        CHECK((launch_multi<true, Conv3DJob, ScalarsJob>(s, da, dim3(std::min(B, 2 * h->cus)), h->scalars_args,
-                                                          dim3(1), 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
-        h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_SCALARS;   // the reduction rode on this launch
-        h->pend_scalars = false;
-      } else {
-        CHECK(launch_conv3<true>(h, s, BA3C_K_CONV3_DGRAD, da));
-      }
       const int gx = conv3_wgrad_p(B, h->cus);
-      {
-        ProbeScope ps(h, s, BA3C_K_CONV3_WGRAD);
-        hipLaunchKernelGGL(conv3_wgrad_kernel, dim3(gx), dim3(512), 0, s,
-                           Conv3WArgs{w.p2, w.dy3, w.part_3, B, w.am(AM_P2, h), w.am(AM_DY3, h)});
+#ifndef BA3C_C3PAIR
+#define BA3C_C3PAIR 1   // 0: A/B build with the small-batch conv3 gradients in two launches
+#endif
+      if (mj && BA3C_C3PAIR) {
+        // small batches: input and weight gradient in one launch (two 256-thread workgroups per
+        // weight-gradient slab; the weight gradient reduces max |dY3| itself, since the input
+        // gradient publishes it only as it runs)
+        const Conv3WArgs wa{w.p2, w.dy3, w.part_3, B, w.am(AM_P2, h), nullptr, 1};
+        CHECK((launch_multi<true, Conv3DJob, Conv3WJob>(s, da, dim3(std::min(B, 2 * h->cus)), wa, dim3(gx, 2),
+                                                         0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
+        h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_CONV3_WGRAD;
+      } else {
+        if (big && h->pend_scalars) {
+          CHECK((launch_multi<true, Conv3DJob, ScalarsJob>(s, da, dim3(std::min(B, 2 * h->cus)), h->scalars_args,
+                                                            dim3(1), 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
+          h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_SCALARS;   // the reduction rode on this launch
+          h->pend_scalars = false;
+        } else {
+          CHECK(launch_conv3<true>(h, s, BA3C_K_CONV3_DGRAD, da));
+        }
+        {
+          ProbeScope ps(h, s, BA3C_K_CONV3_WGRAD);
+          hipLaunchKernelGGL(conv3_wgrad_kernel, dim3(gx), dim3(512), 0, s,
+                             Conv3WArgs{w.p2, w.dy3, w.part_3, B, w.am(AM_P2, h), w.am(AM_DY3, h), 0});
+        }
+        HIP_TRY(hipGetLastError());
       }
-      HIP_TRY(hipGetLastError());
       pl.S = gx;   // one slab per workgroup
     } else {   // BA3C_GENERIC: the fp32-MFMA GEMM engine
       ConvWgrad<false, 7, 7, 64, 3, 3, 64, false> g{w.p2, w.dy3, nullptr, w.part_3, 1.0f, pl.M, pl.N, pl.K, pl.kchunk};

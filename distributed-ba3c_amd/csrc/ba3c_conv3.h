@@ -286,7 +286,6 @@ struct Conv3WG {
   static constexpr int PX = 288, PY = 288, SPB = 128;
   static constexpr int X_BYTES = NPX * PX, Y_BYTES = KP * PY;
   static constexpr int NV4X = NPX * 64 / 4, NV4Y = NPY * 64 / 4;   // float4 per image: 784 / 400
-  static constexpr int XPT = (NV4X + 511) / 512, YPT = (NV4Y + 511) / 512;
 };
 
 struct Conv3WArgs {
@@ -296,35 +295,64 @@ struct Conv3WArgs {
   int batch;
   const uint32_t* amax_x;      // per-image max |p2| slots
   const uint32_t* amax_dy;     // per-image max |dY3| slots
+  int self_dy;                 // 1: max |dY3| reduced from dY3 itself (amax_dy unused)
 };
 
-// bx / gx: first image and image stride; lds: X_BYTES + Y_BYTES; red8: 8 words
-__device__ __forceinline__ void conv3_wgrad_body(const Conv3WArgs& a, int bx, int gx, char* lds, uint32_t* red8) {
+// NT = 512: one workgroup per slab (waves 4..7 take n-blocks 2, 3); NT = 256: two workgroups
+// per slab, n-half `nhw` each (a multi-job launch beside conv3's input gradient: every output
+// element's k order is the same, so the slabs are bit-identical).  bx / gx: first image and
+// image stride; lds: X_BYTES + Y_BYTES; red: NT / 64 words
+template <int NT>
+__device__ __forceinline__ void conv3_wgrad_body(const Conv3WArgs& a, int bx, int gx, int nhw, char* lds, uint32_t* red) {
   using G = Conv3WG;
   using SP = SplitP<2>;
+  constexpr int NW = NT / 64;
+  constexpr int XPT = (G::NV4X + NT - 1) / NT, YPT = (G::NV4Y + NT - 1) / NT;
+  static_assert(NT == 512 || NT == 256, "conv3 weight gradient: 8 or 4 waves");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mg = wave & 3, nh = wave >> 2;
+  const int mg = wave & 3, nh = NT == 512 ? wave >> 2 : nhw;
   char* xs = lds;
   char* ys = lds + G::X_BYTES;
   // whole-tensor scales (the sum runs over images)
-  auto amax8 = [&](const uint32_t* slots) {
-    uint32_t m = 0;
-    for (int i = tid; i < a.batch; i += 512) m = max(m, slots[1 + i]);
+  auto amax_wg = [&](uint32_t m) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
-    if (lane == 0) red8[wave] = m;
+    if (lane == 0) red[wave] = m;
     __syncthreads();
     uint32_t r = 0;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) r = max(r, red8[w]);
+    for (int w = 0; w < NW; ++w) r = max(r, red[w]);
     __syncthreads();
     return r;
   };
-  const int kx = amax_exp(amax8(a.amax_x)), ky = amax_exp(amax8(a.amax_dy));
+  auto amax_slots = [&](const uint32_t* slots) {
+    uint32_t m = 0;
+    for (int i = tid; i < a.batch; i += NT) m = max(m, slots[1 + i]);
+    return amax_wg(m);
+  };
+  // self_dy: max |dY3| over the tensor (the bits of |x| order like the values: the maximum the
+  // input-gradient kernel would publish), four float4 in flight per thread
+  auto amax_dy_self = [&]() {
+    const uint4* y = reinterpret_cast<const uint4*>(a.dy);
+    const int n4 = a.batch * G::NV4Y;
+    uint32_t m = 0;
+    auto m4 = [](uint32_t m, const uint4& v) {
+      return max(max(m, max(v.x & 0x7FFFFFFFu, v.y & 0x7FFFFFFFu)), max(v.z & 0x7FFFFFFFu, v.w & 0x7FFFFFFFu));
+    };
+    int i = tid;
+    for (; i + 3 * NT < n4; i += 4 * NT) {
+      const uint4 v0 = y[i], v1 = y[i + NT], v2 = y[i + 2 * NT], v3 = y[i + 3 * NT];
+      m = m4(m4(m4(m4(m, v0), v1), v2), v3);
+    }
+    for (; i < n4; i += NT) m = m4(m, y[i]);
+    return amax_wg(m);
+  };
+  const int kx = amax_exp(amax_slots(a.amax_x));
+  const int ky = amax_exp(a.self_dy ? amax_dy_self() : amax_slots(a.amax_dy));
   const float xsc = exp2i(kx), ysc = exp2i(ky);
   // dY3 rows 25..31 (the k-step's padding) are zero and never written
-  for (int f = tid; f < (G::KP - G::NPY) * G::PY / 16; f += 512)
+  for (int f = tid; f < (G::KP - G::NPY) * G::PY / 16; f += NT)
     reinterpret_cast<uint4*>(ys + G::NPY * G::PY)[f] = make_uint4(0, 0, 0, 0);
 
   // tr-read lane roles (as wgrad6_body): group g = lane >> 4, K row q, channel quad pq; this
@@ -344,27 +372,33 @@ __device__ __forceinline__ void conv3_wgrad_body(const Conv3WArgs& a, int bx, in
 #pragma unroll
   for (int j = 0; j < 9; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const float4* x4 = reinterpret_cast<const float4*>(a.x);
-  const float4* y4 = reinterpret_cast<const float4*>(a.dy);
-  float4 xv[G::XPT], yv[G::YPT];
+  float4 xv[XPT], yv[YPT];
+  // NT = 256: branch-free (ld4 reads zeros for a rejected element), so the loads stay in flight
+  // together; the 512-thread kernel keeps the selects (branch-free measured 0.0242 -> 0.0256 ms)
   auto load = [&](int img) {
+    const float4* x4 = reinterpret_cast<const float4*>(a.x);
+    const float4* y4 = reinterpret_cast<const float4*>(a.dy);
 #pragma unroll
-    for (int i = 0; i < G::XPT; ++i) {
-      const int f = tid + 512 * i;
-      xv[i] = (img < a.batch && f < G::NV4X) ? x4[(size_t)img * G::NV4X + f] : f4zero();
+    for (int i = 0; i < XPT; ++i) {
+      const int f = tid + NT * i;
+      const bool ok = img < a.batch && f < G::NV4X;
+      if constexpr (NT == 256) xv[i] = ld4(a.x + ((size_t)img * G::NV4X + f) * 4, ok);
+      else xv[i] = ok ? x4[(size_t)img * G::NV4X + f] : f4zero();
     }
 #pragma unroll
-    for (int i = 0; i < G::YPT; ++i) {
-      const int f = tid + 512 * i;
-      yv[i] = (img < a.batch && f < G::NV4Y) ? y4[(size_t)img * G::NV4Y + f] : f4zero();
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + NT * i;
+      const bool ok = img < a.batch && f < G::NV4Y;
+      if constexpr (NT == 256) yv[i] = ld4(a.dy + ((size_t)img * G::NV4Y + f) * 4, ok);
+      else yv[i] = ok ? y4[(size_t)img * G::NV4Y + f] : f4zero();
     }
   };
   load(bx);
   for (int img = bx; img < a.batch; img += gx) {
     __syncthreads();                                     // the previous image's reads are done
 #pragma unroll
-    for (int i = 0; i < G::XPT; ++i) {
-      const int f = tid + 512 * i;
+    for (int i = 0; i < XPT; ++i) {
+      const int f = tid + NT * i;
       if (f < G::NV4X) {
         uint32_t s0[2], s1[2];
         SP::split(xv[i].x, xv[i].y, xsc, s0);
@@ -375,8 +409,8 @@ __device__ __forceinline__ void conv3_wgrad_body(const Conv3WArgs& a, int bx, in
       }
     }
 #pragma unroll
-    for (int i = 0; i < G::YPT; ++i) {
-      const int f = tid + 512 * i;
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + NT * i;
       if (f < G::NV4Y) {
         uint32_t s0[2], s1[2];
         SP::split(yv[i].x, yv[i].y, ysc, s0);
@@ -434,8 +468,17 @@ __device__ __forceinline__ void conv3_wgrad_body(const Conv3WArgs& a, int bx, in
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) conv3_wgrad_kernel(const Conv3WArgs a) {
   __shared__ uint4 lds4[(Conv3WG::X_BYTES + Conv3WG::Y_BYTES) / 16];
   __shared__ uint32_t red8[8];
-  conv3_wgrad_body(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4), red8);
+  conv3_wgrad_body<512>(a, blockIdx.x, gridDim.x, 0, reinterpret_cast<char*>(lds4), red8);
 }
 #endif
+
+// the 256-thread weight gradient as a multi-job launch job: x = slab (first image), y = n-half
+struct Conv3WJob {
+  using Args = Conv3WArgs;
+  static constexpr int LDS = Conv3WG::X_BYTES + Conv3WG::Y_BYTES;
+  __device__ static void run(const Args& a, int x, int y, int, int gx, char* lds, uint32_t* red4) {
+    conv3_wgrad_body<256>(a, x, gx, y, lds, red4);
+  }
+};
 
 }  // namespace ba3c
