@@ -91,18 +91,29 @@ def _free_port():
     return p
 
 
-def spawn_ranks(n, argv, script=None, grace=None):
+SPAWN_TIMEOUT_RC = 124          # every rank killed at the overall deadline (as timeout(1))
+
+
+def spawn_ranks(n, argv, script=None, grace=None, deadline=None):
     """`python bench.py --gpus N` without torchrun: start N rank processes of `script` (this
     file) with the environment torchrun would give them (RANK, LOCAL_RANK, WORLD_SIZE,
     LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), one per local GPU.  This
     process makes no GPU call; the children inherit stdout (rank 0 prints the JSON line).
-    If a rank fails, the others get `grace` seconds (BA3C_SPAWN_GRACE, default 60) to end
-    before they are killed, so a dead peer cannot leave the job hanging in a collective.
-    Returns the worst exit status (a signal s counts as 128 + s)."""
+
+    Two guards, so a hung job ends before the driver's limit: if a rank fails, the others get
+    `grace` seconds (BA3C_SPAWN_GRACE, default 60) to end before they are killed (a dead peer
+    cannot leave rank 0 waiting in a collective); and if the job is still running `deadline`
+    seconds after the start (BA3C_SPAWN_DEADLINE, default 900) every rank is killed — a rank
+    stuck inside a collective never exits, so the grace timer alone would never start.
+    Returns the status of the FIRST rank seen to fail (a signal s counts as 128 + s), not the
+    status of the peers this launcher killed afterwards; SPAWN_TIMEOUT_RC (124) at the
+    deadline; 0 when every rank succeeded."""
     import signal
     import subprocess
     if grace is None:
         grace = float(os.environ.get("BA3C_SPAWN_GRACE", "60"))
+    if deadline is None:
+        deadline = float(os.environ.get("BA3C_SPAWN_DEADLINE", "900"))
     port = _free_port()
     procs = []
     for r in range(n):
@@ -118,24 +129,45 @@ def spawn_ranks(n, argv, script=None, grace=None):
                 p.terminate()
         raise SystemExit(128 + signum)
 
+    def status(rc):
+        return 128 - rc if rc < 0 else rc
+
     old = {s: signal.signal(s, stop) for s in (signal.SIGTERM, signal.SIGINT)}
+    t_start = time.time()
+    first_rc, timed_out = None, False
     try:
         failed_at = None
         while True:
             rcs = [p.poll() for p in procs]
             if all(rc is not None for rc in rcs):
                 break
-            if failed_at is None and any(rc not in (None, 0) for rc in rcs):
-                failed_at = time.time()
-            if failed_at is not None and time.time() - failed_at > grace:
+            if first_rc is None:
+                bad = [rc for rc in rcs if rc not in (None, 0)]
+                if bad:
+                    first_rc, failed_at = status(bad[0]), time.time()
+            now = time.time()
+            if (failed_at is not None and now - failed_at > grace) or now - t_start > deadline:
+                if failed_at is None:
+                    timed_out = True
+                    print("bench: ranks still running %.0f s after the start "
+                          "(BA3C_SPAWN_DEADLINE); killing all" % deadline, file=sys.stderr,
+                          flush=True)
                 for p in procs:
                     if p.poll() is None:
                         p.kill()
+                for p in procs:
+                    p.wait()
+                continue
             time.sleep(0.1)
     finally:
         for s, h in old.items():
             signal.signal(s, h)
-    return max(128 - rc if rc < 0 else rc for rc in rcs)
+    if first_rc is not None:
+        return first_rc
+    if timed_out:
+        return SPAWN_TIMEOUT_RC
+    bad = [status(rc) for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def exchange_selftest(world, rank, iters=5):
@@ -295,6 +327,13 @@ def exchange_report(tr, batch, timeline, iters, world):
     so the cost of RCCL sharing CUs with the persistent conv kernels shows per launch."""
     opt, eng = tr.optimizer, tr.engine
     tb, off = eng.bucket_split()
+    rccl_comms = None
+    if dist.is_initialized():
+        info = opt.rccl_info() if hasattr(opt, "rccl_info") else None
+        if info is not None:
+            info["torch_device"] = torch.cuda.current_device()
+        rccl_comms = [None] * dist.get_world_size()
+        dist.all_gather_object(rccl_comms, info)
     total = eng.grads.numel()
     tl = timeline.summary()
     names = sorted(k for k in tl if k.endswith("_ms"))
@@ -331,7 +370,10 @@ def exchange_report(tr, batch, timeline, iters, world):
             "phase2_launch_ms": {k: {"with_exchange": round(a, 4), "exchange_off": round(b, 4)}
                                  for k, a, b in zip(PHASE2_KERNELS, el[len(names):len(names) + n],
                                                     el[len(names) + n:])},
-            "probe_iters": iters}
+            "probe_iters": iters,
+            # what RCCL itself reports on every rank (rank count, own rank, HIP device, PCI
+            # bus id): world ranks on world distinct devices
+            "rccl_comms": rccl_comms}
 
 
 def find_dominant_kernel(tr, batch, steps=3):
@@ -438,6 +480,42 @@ def cpu_baseline(F, S, A, big_seconds=10.0, b32_steps=50):
             "b32_value": round(32 / small_med, 2), "b32_ms_per_step": round(small_med * 1000, 2)}
 
 
+def replicas_identical(tensors, group=None):
+    """N > 1: every rank's tensors (parameters, optimizer slots) equal rank 0's bit for bit —
+    the synchronous step's invariant (identical update on identical sums).  Rank 0's copies are
+    broadcast and compared on every rank; the verdict is agreed with a MIN all-reduce, so all
+    ranks return the same bool."""
+    ok = True
+    for t in tensors:
+        ref = t.clone()
+        dist.broadcast(ref, src=0, group=group)
+        ok = ok and bool(torch.equal(ref, t))
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=tensors[0].device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item())
+
+
+def health(out, flags, identical=None):
+    """Write the run's health into the line: the engine's device error flags after the timed
+    steps (ba3c_device_errors: an in-launch wait that gave up makes the parameters invalid)
+    and, for N > 1, whether the replicas stayed bit-identical.  Returns the process status:
+    non-zero when either check failed, so a wrong run cannot pass as a valid line."""
+    from ba3c_amd.trainer import Ba3cTrainer
+    out["device_errors"] = int(flags)
+    if flags:
+        out["device_errors_what"] = Ba3cTrainer.describe_device_errors(flags)
+    if identical is not None:
+        out["replicas_identical"] = bool(identical)
+    return 1 if flags or identical is False else 0
+
+
+ARITH = ("fp32-class products on 16-bit MFMA with fp32 accumulation: conv0 u8 x fp16 hi/lo "
+         "(2 products), conv0..conv3 power-of-two-scaled fp16 hi/lo (3 products: hi*hi + hi*lo "
+         "+ lo*hi), fc1 / heads weight gradient bf16 hi/mid/lo (6 products); per product ~2^-20 "
+         "relative (fp32 rounding 2^-24), normwise per tensor; elements below ~2^-17 of their "
+         "image's / tensor's max |x| lose fp16 bits (DESIGN.md §3.1)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -508,6 +586,11 @@ def run_rank(args, world, rank, local):
     elapsed, med_ms = time_steps(tr, batch, args.steps, args.warmup, world, probe=dom)
     probe_ms, launches = tr.engine.probe_read()
     tr.engine.probe_enable(None)
+    flags = tr.engine.device_errors()     # synchronises; after the timed region
+    identical = None
+    if world > 1:
+        inner = tr.optimizer._opt if hasattr(tr.optimizer, "_opt") else tr.optimizer
+        identical = replicas_identical([tr.engine.params] + list(inner.slots or []))
     if timeline is not None:
         # keep only the timed steps' events
         timeline.steps = timeline.steps[-args.steps:]
@@ -552,6 +635,7 @@ def run_rank(args, world, rank, local):
            "ms_per_step_median": round(med_ms, 4),
            "value_median": round(world * B / (med_ms / 1000.0), 1),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "arith": ARITH,
            "data": "synthetic uint8 84x84x4 frames, random actions/returns, weights from the "
                    "reference initialisers (seed 0); resident in HBM",
            "config": {"workload": "configs[2]/[3]: BA3C train step (fwd+bwd+clip+%sAdam) "
@@ -563,18 +647,20 @@ def run_rank(args, world, rank, local):
                                    "unfused update)" if sync else "fused single replica",
                       "backup_workers": 0},
            "step_tflops_algorithmic": round(step_tflops, 2),
-           "step_vs_fp32_mfma_peak": round(step_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
            "ceiling": ceiling,
            "roofline": roof,
            "probe": {"kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": launches},
            "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()}}
 
+    rc = health(out, flags, identical)
     if sync:
         out["exchange"] = exchange_report(tr, batch, timeline, max(args.steps // 3, 5), world)
     if not args.no_overlap:
         out["overlap"] = overlap_bench(tr, batch, args.predict_batch, 10, world)
     if not args.no_b32:
+        close_exchange(tr)
         del tr
+        tr = None
         tr32, b32 = build_trainer(32, 128, 4, A, world, seed=rank, sync=sync)
         n32 = max(args.steps, 100)
         el32, med32 = time_steps(tr32, b32, n32, 10, world)
@@ -586,6 +672,11 @@ def run_rank(args, world, rank, local):
             elg = time_graph_steps(tr32, b32, n32, 10)
             out["b32"].update({"value_graph": round(32 * n32 / elg, 1),
                                "ms_per_step_graph": round(elg / n32 * 1000.0, 4)})
+        f32 = tr32.engine.device_errors()
+        if f32:
+            out["b32"]["device_errors"] = int(f32)
+            rc = 1
+        tr = tr32
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(F, S, A, args.cpu_seconds)
         out["gpu_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
@@ -593,8 +684,15 @@ def run_rank(args, world, rank, local):
         print(json.dumps(out), flush=True)
     if sync:
         dist.barrier()
+        close_exchange(tr)
         dist.destroy_process_group()
-    return 0
+    return rc
+
+
+def close_exchange(tr):
+    """Destroy the trainer's direct RCCL communicator (before its process group goes)."""
+    if tr is not None and hasattr(tr.optimizer, "close"):
+        tr.optimizer.close()
 
 
 if __name__ == "__main__":

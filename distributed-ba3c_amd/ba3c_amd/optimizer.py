@@ -364,23 +364,71 @@ class SyncReplicasOptimizer(object):
 
     def direct_rccl(self, device):
         """The direct RCCL communicator of this group (created on first use, collectively), or
-        None on a gloo group or with BA3C_DIRECT_RCCL=0."""
+        None on a gloo group or with BA3C_DIRECT_RCCL=0.
+
+        Every rank takes the same path: the library load, the communicator and an
+        exact-sum self-test through it are each agreed on with a MIN all-reduce over the
+        process group, so one rank falling back to torch's collective while the others wait on
+        the direct communicator cannot happen."""
         flag = os.environ.get("BA3C_DIRECT_RCCL", "1")
         if flag not in ("0", "1"):
             raise ValueError("BA3C_DIRECT_RCCL must be 0 or 1 (got %r)" % flag)
         if flag == "0" or dist.get_backend(self.group) != "nccl" or self._rccl is False:
             return None
         if self._rccl is None:
-            from .rccl import RcclComm, RcclError
+            from . import rccl as R
+
+            def agree(ok, what):
+                t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+                if int(t.item()) == 0:
+                    print("ba3c: direct RCCL unavailable on some rank (%s); every rank uses "
+                          "torch's collective" % what, file=sys.stderr)
+                    return False
+                return True
+            err = None
             try:
-                self._rccl = RcclComm(self.group, device)
-            except (OSError, AttributeError, RcclError) as e:
-                # the library or the communicator is unavailable: torch's collective does the
-                # same sums (every rank raises alike, ncclCommInitRank being collective)
-                print("ba3c: direct RCCL unavailable (%s); using torch's collective" % e, file=sys.stderr)
+                R._lib()
+            except (OSError, AttributeError) as e:
+                err = e
+            if not agree(err is None, "library: %s" % err):
                 self._rccl = False
                 return None
+            comm = None
+            try:
+                comm = R.RcclComm(self.group, device)
+                ok = comm.selftest()
+                err = None if ok else "exact-sum self-test mismatch"
+            except R.RcclError as e:
+                err = e
+            if not agree(err is None, "communicator: %s" % err):
+                if comm is not None:
+                    comm.close()
+                self._rccl = False
+                return None
+            self._rccl = comm
+            import atexit
+            atexit.register(self.close)
         return self._rccl
+
+    def rccl_info(self):
+        """RcclComm.info() of the direct communicator, or None when torch's collective runs."""
+        return self._rccl.info() if self._rccl else None
+
+    def close(self):
+        """Destroy the direct RCCL communicator (before dist.destroy_process_group; also run at
+        interpreter exit), so no RCCL proxy thread outlives the process group."""
+        if self._rccl:
+            torch.cuda.synchronize(self._rccl.device)
+            self._rccl.close()
+            self._rccl = None
+
+    # HIP event recorded on the exchange stream after the last asynchronous bucket sum of the
+    # step; the next sum on the same communicator from another stream waits for it, so the
+    # order of two collectives on one communicator never rests on RCCL's cross-stream
+    # serialisation (VERDICT r04 item 2b)
+    _ar_done = None
+    _ar_event = None
 
     def aggregate_bucket_async(self, engine, t0, t1, off0, off1, marks=None, last=False):
         """Clip tensors [t0, t1) and start the RCCL sum of flat range [off0, off1); returns
@@ -401,6 +449,9 @@ class SyncReplicasOptimizer(object):
             return self._all_reduce(buf, async_op=True)
         rccl = self.direct_rccl(buf.device)
         if rccl is not None and last:
+            if self._ar_done is not None:
+                cur.wait_event(self._ar_done)     # the exchange stream's sum is enqueued first
+                self._ar_done = None
             if begin is not None:
                 begin.record(cur)
             rccl.all_reduce_sum(buf, cur)
@@ -418,6 +469,10 @@ class SyncReplicasOptimizer(object):
                 return _StagedWork(work, host, buf, stream=comm, end=end)
             if rccl is not None:
                 rccl.all_reduce_sum(buf, comm)
+                if self._ar_event is None:
+                    self._ar_event = torch.cuda.Event()
+                self._ar_event.record(comm)
+                self._ar_done = self._ar_event
             else:
                 work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                 work.wait()                   # `comm` waits for the collective's stream

@@ -127,8 +127,9 @@ class MultiThreadAsyncPredictor(object):
         probs, value = out[0], out[1]
         eng = self.predictor.engine
         with self.predictor.on_stream():        # sampling reads probs on the stream that wrote them
-            u = torch.from_numpy(np.array([self.rs.random_sample() for _ in range(len(states))],
-                                          dtype=np.float64)).to(eng.device)
+            # one MT19937 double per state, drawn in one call: the same stream as len(states)
+            # scalar random_sample() calls (train.py:382 draws one per np.random.choice)
+            u = torch.from_numpy(self.rs.random_sample(len(states))).to(eng.device)
             actions, flag = eng.sample(probs, u)
             f = int(flag.item())
             if f & 1:

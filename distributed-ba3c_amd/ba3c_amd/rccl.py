@@ -44,6 +44,9 @@ def _lib():
         lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        for fn in ("ncclCommCount", "ncclCommCuDevice", "ncclCommUserRank"):
+            getattr(lib, fn).argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        lib.ncclGetVersion.argtypes = [ctypes.POINTER(ctypes.c_int)]
         _LIB = lib
     return _LIB
 
@@ -78,6 +81,40 @@ class RcclComm(object):
         with torch.cuda.device(self.device):
             _check(lib.ncclCommInitRank(ctypes.byref(self._comm), self.world, uid, self.rank),
                    "ncclCommInitRank")
+
+    def info(self):
+        """What RCCL itself reports for this communicator: its rank
+        count, this rank's position and the HIP device it drives, plus that device's PCI bus
+        id and the RCCL version — world ranks on world distinct devices is what a multi-GPU
+        line must show."""
+        lib = _lib()
+        out = {}
+        for key, fn in (("comm_count", "ncclCommCount"), ("comm_user_rank", "ncclCommUserRank"),
+                        ("comm_device", "ncclCommCuDevice")):
+            v = ctypes.c_int(-1)
+            _check(getattr(lib, fn)(self._comm, ctypes.byref(v)), fn)
+            out[key] = v.value
+        ver = ctypes.c_int(0)
+        _check(lib.ncclGetVersion(ctypes.byref(ver)), "ncclGetVersion")
+        out["rccl_version"] = ver.value
+        props = torch.cuda.get_device_properties(out["comm_device"])
+        out["pci_bus_id"] = "%04x:%02x:%02x" % (getattr(props, "pci_domain_id", 0),
+                                                getattr(props, "pci_bus_id", 0),
+                                                getattr(props, "pci_device_id", 0))
+        return out
+
+    def selftest(self):
+        """One exact in-place sum through this communicator on the caller's current stream:
+        rank r contributes (r + 1) * i for i < 4096 (small integers, exact in fp32 in any
+        summation order), so every element must equal i * world * (world + 1) / 2.  Returns
+        True when it does (the caller makes the keep/fallback decision collectively)."""
+        n = 4096
+        i = torch.arange(n, dtype=torch.float32, device=self.device)
+        buf = i * float(self.rank + 1)
+        stream = torch.cuda.current_stream(self.device)
+        self.all_reduce_sum(buf, stream)
+        stream.synchronize()
+        return bool(torch.equal(buf, i * float(self.world * (self.world + 1) // 2)))
 
     def all_reduce_sum(self, buf, stream):
         """In-place sum of the contiguous fp32 device tensor `buf` over the group, enqueued on

@@ -85,16 +85,29 @@ class Ba3cTrainer(object):
         for p in self._procs:
             p.process(self.engine)
 
+    @staticmethod
+    def describe_device_errors(flags):
+        """Decode ba3c_device_errors' bits (include/ba3c.h)."""
+        what = []
+        if flags & 1:
+            what.append("bit 0: the fused clip + update launch applied a clip factor from stale "
+                        "partials (rerun with BA3C_FUSED_UPDATE=0)")
+        if flags & 2:
+            what.append("bit 1: a one-launch bucket clip (ba3c_clip_grads_range) gave up waiting, "
+                        "so invalid clipped gradients entered the all-reduce")
+        if flags & ~3:
+            what.append("unknown bits 0x%x" % (flags & ~3))
+        return "; ".join(what)
+
     def check_device_errors(self):
-        """Abort on an in-launch wait that gave up (ba3c_device_errors != 0): the fused
-        clip + update kernel then applied a clip factor from stale partials, so the parameters
-        are no longer the reference's.  Called where the host already synchronises (run_step,
-        the metrics flush of train.py); it synchronises the device itself."""
+        """Abort on an in-launch wait that gave up (ba3c_device_errors != 0): the parameters
+        are then no longer the reference's.  Called where the host already synchronises
+        (run_step, the metrics flush of train.py, bench.py after the timed steps); it
+        synchronises the device itself."""
         f = self.engine.device_errors() if hasattr(self.engine, "device_errors") else 0
         if f:
-            raise RuntimeError("device error flags 0x%x after global step %d: an in-launch "
-                               "grid wait gave up (fused clip + update); rerun with "
-                               "BA3C_FUSED_UPDATE=0" % (f, self.global_step))
+            raise RuntimeError("device error flags 0x%x after global step %d: %s"
+                               % (f, self.global_step, self.describe_device_errors(f)))
 
     def train_step(self, state, action, futurereward):
         """Device-side step (used by bench.py).  No host synchronisation, except with backup

@@ -31,7 +31,7 @@
 using namespace ba3c;
 
 // The TfDictOp scalar reduction (scalars_block) as one workgroup of a multi-job launch: at
-// large batches it rides on conv3's weight-gradient launch instead of its own dependent
+// large batches it rides on conv3's input-gradient launch instead of its own dependent
 // launch after the heads (nothing in the step reads the scalars).
 struct ScalarsJob {
   struct Args {
@@ -96,9 +96,11 @@ struct ba3c_handle {
   // gradient, (1) conv1's input gradient, or (0) runs alone (BA3C_C1PAIR)
   int c1pair = 2;
   uint32_t merged[BA3C_NUM_KERNELS] = {};   // ba3c_kernel_merged, per training pass
-  // large-batch scalar reduction deferred from run_heads onto conv3's weight-gradient launch
-  // (one-pass backward only; default; BA3C_SCALARS_RIDE=0: its own launch after the heads).
-  // r04 same-box A/B: step 1.954 -> 1.935 ms, conv3's weight-gradient launch +1.6 us
+  // large-batch (B > OVERLAP_B) scalar reduction deferred from run_heads onto conv3's
+  // input-gradient launch as one extra workgroup (default; also across the phase-1/phase-2
+  // split of the N>1 step); when no launch takes it, finish() launches it at the end of phase
+  // 0 or phase 2.  BA3C_SCALARS_RIDE=0: its own launch after the heads.
+  // r04 same-box A/B: step 1.954 -> 1.935 ms
   bool scalars_ride = true;
   bool pend_scalars = false;
   ScalarsJob::Args scalars_args{};
@@ -747,7 +749,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   // join the side stream and run the deferred reductions of this phase in one launch
   auto finish = [&]() -> int {
     if (h->pend_scalars && phase != 1) {   // no launch took the deferred scalar reduction
-      // (phase 1 leaves it pending: conv3's weight-gradient launch in phase 2 takes it)
+      // (phase 1 leaves it pending: conv3's input-gradient launch in phase 2 takes it)
       const ScalarsJob::Args& sa = h->scalars_args;
       ProbeScope ps(h, s, BA3C_K_SCALARS);
       hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, sa.terms, sa.B, sa.beta, sa.relu, sa.out);
@@ -1091,7 +1093,7 @@ int run_heads(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& 
   HIP_TRY(hipGetLastError());
   if (train && scalars && !fuse_scalars && defer_scalars) {
     h->scalars_args = ScalarsJob::Args{w.terms, B, beta, w.relu, scalars};
-    h->pend_scalars = true;      // launched by run_backward (conv3's weight gradient or finish)
+    h->pend_scalars = true;      // launched by run_backward (conv3's input gradient or finish)
   } else if (train && scalars && !fuse_scalars) {
     ProbeScope ps(h, s, BA3C_K_SCALARS);
     hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(256), 0, s, w.terms, B, beta, w.relu, scalars);

@@ -82,7 +82,7 @@ extern "C" {
 #define BA3C_K_WGRAD_REDUCE 16
 #define BA3C_K_CLIP 17
 #define BA3C_K_UPDATE 18
-#define BA3C_K_SCALARS 19   /* TfDictOp scalar reduction (its own launch or a job of conv3's weight gradient) */
+#define BA3C_K_SCALARS 19   /* TfDictOp scalar reduction (its own launch or a job of conv3's input-gradient launch) */
 #define BA3C_NUM_KERNELS 20
 
 typedef struct ba3c_handle ba3c_handle;

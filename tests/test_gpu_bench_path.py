@@ -173,7 +173,14 @@ def test_sync_replicas_rccl_allreduce_world1_equals_single_replica_step(monkeypa
         got = run(True)
         assert bool(opts[0]._rccl) == (direct == "1")
         if opts[0]._rccl:
-            opts[0]._rccl.close()
+            # what the N>1 line's exchange object records from every rank
+            info = opts[0].rccl_info()
+            assert info["comm_count"] == 1 and info["comm_user_rank"] == 0
+            assert info["comm_device"] == torch.cuda.current_device()
+            assert info["rccl_version"] > 0 and ":" in info["pci_bus_id"]
+            assert opts[0]._rccl.selftest()
+            opts[0].close()
+            assert opts[0]._rccl is None
     finally:
         dist.destroy_process_group()
     np.testing.assert_array_equal(got, ref)

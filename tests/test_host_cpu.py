@@ -326,8 +326,60 @@ def test_bench_spawner_returns_the_failing_rank_status(tmp_path):
     import time
     t0 = time.time()
     rc = bench.spawn_ranks(3, [], script=str(script), grace=1.0)
-    assert rc == 128 + 9 or rc == 3, rc          # rank 0 killed (SIGKILL) after rank 1's 3
+    assert rc == 3, rc          # rank 1's own status, not rank 0's SIGKILL from the launcher
     assert time.time() - t0 < 60
     ok = tmp_path / "ok.py"
     ok.write_text("import os; assert os.environ['WORLD_SIZE'] == '2'\n")
     assert bench.spawn_ranks(2, [], script=str(ok), grace=1.0) == 0
+
+
+def test_bench_spawner_deadline_kills_a_hung_job(tmp_path):
+    """Ranks that never exit (a rank stuck inside a collective) are all killed at the overall
+    deadline (BA3C_SPAWN_DEADLINE) and the launcher exits non-zero (124, as timeout(1))."""
+    import time
+    import bench
+    script = tmp_path / "hang.py"
+    script.write_text("import time\ntime.sleep(600)\n")
+    t0 = time.time()
+    rc = bench.spawn_ranks(2, [], script=str(script), grace=60.0, deadline=2.0)
+    assert rc == bench.SPAWN_TIMEOUT_RC, rc
+    assert time.time() - t0 < 30
+
+
+def _replica_worker(rank, world, port, out, perturb):
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = torch.arange(1000, dtype=torch.float32) * 0.37
+        m = torch.ones(1000)
+        if perturb and rank == world - 1:
+            m[517] = torch.nextafter(m[517], torch.tensor(2.0))   # one ulp on one rank
+        out[rank] = bench.replicas_identical([p, m])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("perturb", [False, True])
+def test_bench_replica_identity_check_world2(perturb):
+    """bench.py's N>1 replica check: every rank agrees, and one ulp of
+    difference in one slot of one rank makes every rank report False."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_replica_worker, args=(world, _free_port(), out, perturb), nprocs=world, join=True)
+    assert out[0] == out[1] == (not perturb)
+
+
+def test_bench_health_flags_make_the_run_fail():
+    """bench.py writes ba3c_device_errors' flags into the line and returns a non-zero status
+    for a non-zero flag or diverged replicas."""
+    import bench
+    out = {}
+    assert bench.health(out, 0, None) == 0 and out["device_errors"] == 0
+    out = {}
+    assert bench.health(out, 2, True) == 1
+    assert out["device_errors"] == 2 and "bucket clip" in out["device_errors_what"]
+    assert out["replicas_identical"] is True
+    out = {}
+    assert bench.health(out, 0, False) == 1 and out["replicas_identical"] is False

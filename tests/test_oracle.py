@@ -215,3 +215,30 @@ def test_torch_cpu_baseline_restatement_matches_oracle():
         if mask.any():
             e = np.abs(d_got[mask] - d_ref[mask]).max() / np.abs(d_ref[mask]).max()
             assert e < 1e-4, (k, e)
+
+
+@pytest.mark.parametrize("frames", ["random", "atari"])
+def test_torch_f64_forced_restatement_matches_oracle(frames):
+    """oracle/ba3c_torch_f64.py (the checker of the B=2048 GPU test) against the numpy oracle:
+    the same forced decisions (the oracle's own, so both follow one routing), every gradient
+    and the cost to ~1e-12; its own_decisions() equal the oracle's own codes and ReLU signs."""
+    from atari_frames import atari_frames
+    from oracle.ba3c_torch_f64 import loss_and_grads_forced, own_decisions
+    B = 6
+    rs = np.random.RandomState(9)
+    p32 = O.init_params(512, 1, 4, seed=2, dtype=np.float32)
+    params = {k: v.astype(np.float64) for k, v in p32.items()}
+    state = (atari_frames(B, 3) if frames == "atari"
+             else rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8))
+    action = rs.randint(0, 4, size=B)
+    R = rs.normal(size=B)
+    cfg = {"fc_neurons": 512, "fc_splits": 1}
+    t, s, g = O.loss_and_grads_chunked(params, state, action, R, cfg, chunk=4)
+    forced = {"c0": t["own_c0"], "c1": t["own_c1"], "c2": t["own_c2"], "a3_mask": t["a3_pos"]}
+    g2, out = loss_and_grads_forced(params, state, action, R, cfg, forced, chunk=4)
+    for k in g:
+        assert np.abs(g[k] - g2[k]).max() <= 1e-11 * np.abs(g[k]).max(), k
+    assert abs(out["cost"] - s["cost"]) <= 1e-12 * max(1.0, abs(s["cost"]))
+    own = own_decisions(p32, state, chunk=4)
+    for k in ("c0", "c1", "c2", "a3_mask"):
+        np.testing.assert_array_equal(own[k], forced[k])
