@@ -344,26 +344,46 @@ struct Wg6WGeom {
 // conv1's whole-channel weight-gradient geometry (ba3c_capi.hip Lay<2>::W1W, ba3c_conv0.hip)
 using Conv1W6W = Wg6WGeom<40, 40, 32, 32, 4, 160, 160>;
 
+// Work units of a workgroup: (tap, c-block) pairs u = 2 tap + cb, 50 of them for 25 taps x 2
+// c-blocks; a unit's A fragments feed both n-blocks (6 MFMAs per k-step).  Wave w owns units
+// [U0, U0 + NU).  BA3C_W6W_BAL=1 (default): 13 / 13 / 12 / 12 units — the r03/r04 split was
+// whole taps, 7 / 6 / 6 / 6 = 14 / 12 / 12 / 12 units, and every band waited for the 14-unit
+// wave (25 / 28 of the MFMA pipes busy).  Per output the k-order is unchanged, so the slabs
+// are bit-identical either way.
+#ifndef BA3C_W6W_BAL
+#define BA3C_W6W_BAL 1
+#endif
+#ifndef BA3C_W6W_PF
+#define BA3C_W6W_PF 1
+#endif
 template <class G>
-__device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
+struct Wg6WUnits {
+  static constexpr int UNITS = G::NTAP * G::CB;
+  static constexpr int BASE = UNITS / 4, REM = UNITS % 4;
+  __host__ __device__ static constexpr int u0(int w) {
+    return BA3C_W6W_BAL ? w * BASE + (w < REM ? w : REM)
+                        : G::CB * (w * G::TBASE + (w < G::TREM ? w : G::TREM));
+  }
+  __host__ __device__ static constexpr int nu(int w) { return u0(w + 1) - u0(w); }
+  static constexpr int MAXU = BA3C_W6W_BAL ? BASE + (REM > 0) : G::CB * G::TW;
+};
+
+template <class G, int U0, int NU>
+__device__ __forceinline__ void wgrad6w_units(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
   using SP = SplitP<G::NS>;
   const int kx = amax_exp(amax_all(a.amax_x, a.batch, red4));
   const int ky = amax_exp(amax_all(a.amax_dp, a.batch, red4));
   const float xsc = exp2i(kx), ysc = exp2i(ky);
   char* ys = xs + G::X_BYTES;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tap0 = wave * G::TBASE + min(wave, G::TREM);
-  const int ntap = G::TBASE + (wave < G::TREM);
+  const int tid = threadIdx.x, lane = tid & 63;
   const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
   const int kperm = 16 * (g >> 1) + 4 * (g & 1) + q;      // + 8 r for read r (wgrad6_body)
 
-  f32x4 acc[G::TW][G::CB][G::NB];
+  f32x4 acc[NU][G::NB];
 #pragma unroll
-  for (int t = 0; t < G::TW; ++t)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
-    for (int cb = 0; cb < G::CB; ++cb)
-#pragma unroll
-      for (int nb = 0; nb < G::NB; ++nb) acc[t][cb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = 0; nb < G::NB; ++nb) acc[u][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   constexpr int XQ = G::CIN / 4;                          // float4 per X pixel
   constexpr int XPT = G::RB * G::WS * XQ / 256;           // float4 of RB rows per thread
@@ -517,50 +537,100 @@ __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, c
       load_x(ni, nbi * G::RB + G::HALO, xv);
       load_y(ni, nbi);
     }
-#pragma unroll 1
-    for (int s = 0; s < G::KS; ++s) {
-      int xb[2], yb[2];
+    // software-pipelined k-steps: unit u + 1's A fragments are read before unit u's MFMAs, and
+    // during the last unit of a k-step the next k-step's B fragments and its first unit's A
+    // fragments (r04 ISA: each tap's reads were issued ~2 MFMAs ahead of their use and every
+    // k-step opened with a full LDS round trip, at one wave per SIMD nothing hid them)
+    int xb[2];
+    auto addr = [&](int s, int (&xbo)[2], int (&ybo)[2]) {
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         int p = 32 * s + kperm + 8 * r;
-        yb[r] = p * G::PY + 8 * pq;
+        ybo[r] = p * G::PY + 8 * pq;
         if (p >= G::KP) p = 0;                            // padded pixels: dY is zero
         const int y = p / G::WO, x = p - y * G::WO;
-        xb[r] = (y * G::WS + x) * G::PX + 8 * pq;
+        xbo[r] = (y * G::WS + x) * G::PX + 8 * pq;
       }
-      u32x4 b[G::NB][G::NS];
+    };
+    auto read_b = [&](const int (&ybo)[2], u32x4 (&bo)[G::NB][G::NS]) {
 #pragma unroll
       for (int nb = 0; nb < G::NB; ++nb)
 #pragma unroll
         for (int sp = 0; sp < G::NS; ++sp) {
-          const uint2 u0 = lds_tr16(ys + yb[0] + nb * 32 + sp * G::YSB);
-          const uint2 u1 = lds_tr16(ys + yb[1] + nb * 32 + sp * G::YSB);
-          b[nb][sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
+          const uint2 u0 = lds_tr16(ys + ybo[0] + nb * 32 + sp * G::YSB);
+          const uint2 u1 = lds_tr16(ys + ybo[1] + nb * 32 + sp * G::YSB);
+          bo[nb][sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
         }
+    };
+    auto read_a = [&](int u, const int (&xbo)[2], u32x4 (&av)[G::NS]) {
+      const int unit = U0 + u, tap = unit / G::CB, cb = unit - tap * G::CB;
+      const int kh = tap / G::KW, kw = tap - kh * G::KW;
+      const int off = (kh * G::WS + kw) * G::PX + cb * 32;   // compile-time
 #pragma unroll
-      for (int t = 0; t < G::TW; ++t) {
-        if (t >= ntap) break;
-        const int tap = tap0 + t;
-        const int kh = tap / G::KW, kw = tap - kh * G::KW;
-        const int toff = (kh * G::WS + kw) * G::PX;
-        u32x4 av[G::CB][G::NS];
+      for (int sp = 0; sp < G::NS; ++sp) {
+        const uint2 u0 = lds_tr16(xs + xbo[0] + off + sp * G::XSB);
+        const uint2 u1 = lds_tr16(xs + xbo[1] + off + sp * G::XSB);
+        av[sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
+      }
+    };
+    // D: units of lookahead for the A fragments (BA3C_W6W_PF, A/B)
+    constexpr int D = BA3C_W6W_PF, NBUF = D + 1;
+    static_assert(D >= 1 && D < NU, "prefetch distance");
+    u32x4 b[G::NB][G::NS], bn[G::NB][G::NS], avb[NBUF][G::NS];
+    {
+      int yb[2];
+      addr(0, xb, yb);
+      read_b(yb, b);
 #pragma unroll
-        for (int cb = 0; cb < G::CB; ++cb)
+      for (int j = 0; j < D; ++j) read_a(j, xb, avb[j]);
+    }
+    // one k-step; PF: prefetch the next k-step's B and first D units' A fragments (all but
+    // the last k-step of a band)
+    auto kstep = [&](int s, auto pf) {
+      constexpr bool PF = decltype(pf)::value;
+      int xbn[2], ybn[2];
 #pragma unroll
-          for (int sp = 0; sp < G::NS; ++sp) {
-            const uint2 u0 = lds_tr16(xs + xb[0] + toff + sp * G::XSB + cb * 32);
-            const uint2 u1 = lds_tr16(xs + xb[1] + toff + sp * G::XSB + cb * 32);
-            av[cb][sp] = u32x4{u0.x, u0.y, u1.x, u1.y};
+      for (int u = 0; u < NU; ++u) {
+        const int v = u + D;                              // the unit whose A is read now
+        if (v < NU) {
+          read_a(v, xb, avb[v % NBUF]);
+        } else if (PF) {
+          if (v == NU) {
+            addr(s + 1, xbn, ybn);
+            read_b(ybn, bn);
           }
+          read_a(v - NU, xbn, avb[v % NBUF]);
+        }
+        __builtin_amdgcn_sched_barrier(0);                // keep those reads ahead of the MFMAs
+        const u32x4 (&av)[G::NS] = avb[u % NBUF];
 #pragma unroll
         for (int pr = 0; pr < SP::NPROD; ++pr)
 #pragma unroll
-          for (int cb = 0; cb < G::CB; ++cb)
-#pragma unroll
-            for (int nb = 0; nb < G::NB; ++nb)
-              acc[t][cb][nb] = SP::mfma(av[cb][SP::pa(pr)], b[nb][SP::pb(pr)], acc[t][cb][nb]);
+          for (int nb = 0; nb < G::NB; ++nb)
+            acc[u][nb] = SP::mfma(av[SP::pa(pr)], b[nb][SP::pb(pr)], acc[u][nb]);
       }
-    }
+      if (PF) {
+#pragma unroll
+        for (int nb = 0; nb < G::NB; ++nb)
+#pragma unroll
+          for (int sp = 0; sp < G::NS; ++sp) b[nb][sp] = bn[nb][sp];
+        xb[0] = xbn[0];
+        xb[1] = xbn[1];
+        // the next step's units 0 .. D - 1 were read into buffers NU % NBUF ..: rotate
+        u32x4 t[D][G::NS];
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+#pragma unroll
+          for (int sp = 0; sp < G::NS; ++sp) t[j][sp] = avb[(NU + j) % NBUF][sp];
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+#pragma unroll
+          for (int sp = 0; sp < G::NS; ++sp) avb[j][sp] = t[j][sp];
+      }
+    };
+#pragma unroll 1
+    for (int s = 0; s + 1 < G::KS; ++s) kstep(s, std::true_type{});
+    kstep(G::KS - 1, std::false_type{});
   }
 
   // ---- epilogue: one full slab per workgroup (lane: column o = 16 nb + (lane & 15), rows
@@ -568,20 +638,29 @@ __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, c
   float* pz = a.part + (size_t)bx * G::M * G::COUT;
   const float us1 = exp2i(-kx), us2 = exp2i(-ky);
 #pragma unroll
-  for (int t = 0; t < G::TW; ++t) {
-    if (t >= ntap) break;
-    const int tap = tap0 + t;
+  for (int u = 0; u < NU; ++u) {
+    const int unit = U0 + u, tap = unit / G::CB, cb = unit - tap * G::CB;
 #pragma unroll
-    for (int cb = 0; cb < G::CB; ++cb)
+    for (int nb = 0; nb < G::NB; ++nb) {
+      const int o = nb * 16 + (lane & 15);
 #pragma unroll
-      for (int nb = 0; nb < G::NB; ++nb) {
-        const int o = nb * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = cb * 16 + 4 * (lane >> 4) + r;
-          pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[t][cb][nb][r] * us1 * us2;
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int c = cb * 16 + 4 * (lane >> 4) + r;
+        pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[u][nb][r] * us1 * us2;
       }
+    }
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
+  using U = Wg6WUnits<G>;
+  static_assert(U::u0(4) == U::UNITS && U::nu(0) <= U::MAXU, "unit partition");
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: wgrad6w_units<G, U::u0(0), U::nu(0)>(a, bx, gx, xs, red4); break;
+    case 1: wgrad6w_units<G, U::u0(1), U::nu(1)>(a, bx, gx, xs, red4); break;
+    case 2: wgrad6w_units<G, U::u0(2), U::nu(2)>(a, bx, gx, xs, red4); break;
+    default: wgrad6w_units<G, U::u0(3), U::nu(3)>(a, bx, gx, xs, red4); break;
   }
 }
 

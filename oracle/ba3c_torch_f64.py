@@ -5,9 +5,8 @@ the checker; the product path never imports it).
 Why it exists: the numpy oracle (`ba3c_oracle.loss_and_grads_chunked`) needs ~10 s per 128
 samples, too slow for the bench workload itself (B=2048, F=512).  This module computes the same
 function — `OpenAIGym/train.py:164-327` differentiated as `train/multigpu.py:85-86` does — with
-torch's float64 convolutions and autograd, on any device the caller picks (the GPU tests run it
-on the card as a checker: fp64 im2col GEMMs of torch, an implementation independent of the HIP
-kernels).  It is pinned to the numpy oracle by `tests/test_oracle.py` (same forced decisions,
+torch's float64 convolutions and autograd on the CPU (the B=2048 GPU test runs it on the
+host as the checker, ~20 s: an implementation independent of the HIP kernels).  It is pinned to the numpy oracle by `tests/test_oracle.py` (same forced decisions,
 agreement ~1e-12 at small B).
 
 Forced decisions (`forced`, as `ba3c_oracle.loss_and_grads(forced=...)`): the max-pool argmax
@@ -41,33 +40,48 @@ def _pool_forced(z, code):
     return torch.where(dead, torch.zeros_like(p), p)
 
 
-def own_decisions(params, state, chunk=256, device="cpu"):
+def own_decisions(params, state, chunk=256, device="cpu", tol=2e-5):
     """The float64 forward's own discrete decisions (`ba3c_oracle.maxpool2x2_argmax`: first
     maximum in row-major window order, code 255 where the window max <= 0; conv3's ReLU mask),
-    in the workspace's NHWC layouts — to count how often a checked side decided otherwise."""
+    in the workspace's NHWC layouts — to count how often a checked side decided otherwise —
+    and where those decisions are numerically ambiguous (`near_c0`..`near_c2`, `near_a3`:
+    `ba3c_oracle.ambiguous_windows` / `ambiguous_relu` — a competitor not exactly equal to
+    the window max but within tol x the image's max |z| of it, or a max / pre-activation that
+    close to zero without being zero)."""
     dev = torch.device(device)
     C = state.shape[3]
     W = {k: torch.tensor(np.asarray(params[k], np.float64), device=dev).permute(3, 2, 0, 1)
          for k in ("conv0/W", "conv1/W", "conv2/W", "conv3/W")}
     W["conv0/W"] = W["conv0/W"][:, :C]
-    out = {"c0": [], "c1": [], "c2": [], "a3_mask": []}
+    out = {k: [] for k in ("c0", "c1", "c2", "a3_mask", "near_c0", "near_c1", "near_c2",
+                           "near_a3")}
+
+    def image_eps(z):
+        return tol * z.abs().reshape(z.shape[0], -1).max(dim=1).values.reshape(-1, 1, 1, 1)
 
     def pool(z):
         B, Cc, H, Wd = z.shape
         win = z.reshape(B, Cc, H // 2, 2, Wd // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(
             B, Cc, H // 2, Wd // 2, 4)
         mx, code = win.max(dim=4)           # first maximum (torch returns the first index)
+        eps = image_eps(z)
+        gap = mx[..., None] - win
+        near = ((gap > 0) & (gap <= eps[..., None])).any(dim=4) | \
+            ((mx != 0) & (mx.abs() <= eps))
         code = torch.where(mx > 0, code, 255).to(torch.uint8)
-        return torch.relu(mx), code.permute(0, 2, 3, 1)
+        return torch.relu(mx), code.permute(0, 2, 3, 1), near.permute(0, 2, 3, 1)
     with torch.no_grad():
         for lo in range(0, state.shape[0], chunk):
             x = torch.as_tensor(state[lo:lo + chunk], device=dev).to(torch.float64) / 255.0
             p = x.permute(0, 3, 1, 2)
             for i in range(3):
-                p, c = pool(Fn.conv2d(p, W["conv%d/W" % i]))
+                p, c, near = pool(Fn.conv2d(p, W["conv%d/W" % i]))
                 out["c%d" % i].append(c.cpu().numpy())
+                out["near_c%d" % i].append(near.cpu().numpy())
             z3 = Fn.conv2d(p, W["conv3/W"])
             out["a3_mask"].append((z3 > 0).permute(0, 2, 3, 1).cpu().numpy())
+            near3 = (z3 != 0) & (z3.abs() <= image_eps(z3))
+            out["near_a3"].append(near3.permute(0, 2, 3, 1).cpu().numpy())
     return {k: np.concatenate(v) for k, v in out.items()}
 
 

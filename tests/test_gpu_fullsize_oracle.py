@@ -7,7 +7,7 @@ reference graph, train.py:164-327, run on the CPU; pinned to the numpy oracle in
 tests/test_oracle.py), driven by the GPU's own discrete decisions — the max-pool argmax codes
 c0..c2 and conv3's ReLU mask read back from the workspace — so the comparison is of arithmetic
 alone.  Those decisions are separately held to the float64 forward's own: they may differ only
-on fp32 near-ties (< 1e-4 of the windows).  Random frames and Atari-like frames (exact ties
+on numerically ambiguous windows (fp32 near-ties; exact ties must match).  Random frames and Atari-like frames (exact ties
 everywhere, tests/atari_frames.py)."""
 import numpy as np
 import pytest
@@ -51,11 +51,18 @@ def test_bench_workload_every_gradient_matches_fp64(frames):
     del eng
     torch.cuda.synchronize()
 
+    # the GPU's decisions equal the fp64 forward's own in every window that is not numerically
+    # ambiguous (a near-tie or a max within rounding of zero, which any fp32 evaluation may
+    # resolve either way; exact ties are NOT ambiguous: the first-max rule decides them), and
+    # ambiguous windows stay rare (as tests/test_gpu_hard_inputs.py at B <= 512)
     own = own_decisions(params, state)
     for layer in range(3):
-        flips = float(np.mean(own["c%d" % layer] != codes[layer]))
-        assert flips < 1e-4, (layer, flips)
-    assert float(np.mean(own["a3_mask"] != forced["a3_mask"])) < 1e-4
+        near = own["near_c%d" % layer]
+        assert np.mean(near) < 1e-2, (layer, np.mean(near))
+        bad = (own["c%d" % layer] != codes[layer]) & ~near
+        assert not bad.any(), (layer, int(bad.sum()), np.argwhere(bad)[:4])
+    bad = (own["a3_mask"] != forced["a3_mask"]) & ~own["near_a3"]
+    assert not bad.any(), int(bad.sum())
 
     ref, out = loss_and_grads_forced(params, state, action, R, CFG, forced, chunk=256)
     errs = {k: rel(got[k], ref[k]) for k in ref}

@@ -242,3 +242,5 @@ def test_torch_f64_forced_restatement_matches_oracle(frames):
     own = own_decisions(p32, state, chunk=4)
     for k in ("c0", "c1", "c2", "a3_mask"):
         np.testing.assert_array_equal(own[k], forced[k])
+    for k in ("near_c0", "near_c1", "near_c2", "near_a3"):
+        np.testing.assert_array_equal(own[k], t[k])
