@@ -551,6 +551,16 @@ struct Conv0WArgs {
   const uint32_t* amax_dp; // NS = 2: per-image max |dP0| slots
 };
 
+// packed 16-bit halves: 0xFFFF where the half is zero, else 0 — two packed VALU ops (the plain
+// C form of mask16_eq0 is rewritten by the compiler into a compare + select per half)
+__device__ __forceinline__ uint32_t c0w_mask16_eq0(uint32_t d) {
+  uint32_t m;
+  // (the constants go in SGPRs: an inline constant of a packed op is not replicated to the high
+  // half the way the C vector (1, 1) is)
+  asm("v_pk_min_u16 %0, %1, %2\n\tv_pk_add_u16 %0, %0, %3" : "=&v"(m) : "v"(d), "s"(0x00010001u), "s"(0xFFFFFFFFu));
+  return m;
+}
+
 // bx / gx: first band and persistent stride (blockIdx.x / gridDim.x of the plain kernel; a
 // paired launch passes its own); lds: Conv0W<NS>::ALLOC_U4 uint4 of LDS, red4: 4 words
 template <int NS>
@@ -657,10 +667,34 @@ __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, i
       const uint32_t sy = (uint32_t)(r & 1);
       const int e0 = ((r >> 1) * G::COUT + li) * G::PW + (x0 >> 1);
       u32x4 bv[NS][2];
+#ifndef BA3C_C0W_PKMASK
+#define BA3C_C0W_PKMASK 1
+#endif
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int e = e0 + 16 * nt * G::PW;
         const uint32_t cw = *reinterpret_cast<const uint32_t*>(yc8 + e);
+        if constexpr (BA3C_C0W_PKMASK) {
+          // the four windows' codes as 16-bit halves, xor 2 sy: a window's argmax is in this
+          // pixel row at sub-column h exactly when its half equals h (255 ^ 2 sy never does);
+          // m0 / m1 = 0xFFFF halves where it is sub-column 0 / 1 (packed 16-bit compares:
+          // 14 VALU per n-tile for what took a bfe + compare + select per window and mask)
+          const uint32_t sx = sy * 0x00020002u;
+          const uint32_t k01 = __builtin_amdgcn_perm(cw, cw, 0x0C010C00u) ^ sx;
+          const uint32_t k23 = __builtin_amdgcn_perm(cw, cw, 0x0C030C02u) ^ sx;
+          const uint32_t m0a = c0w_mask16_eq0(k01), m1a = c0w_mask16_eq0(k01 ^ 0x00010001u);
+          const uint32_t m0b = c0w_mask16_eq0(k23), m1b = c0w_mask16_eq0(k23 ^ 0x00010001u);
+#pragma unroll
+          for (int sp = 0; sp < NS; ++sp) {
+            const uint2 u = *reinterpret_cast<const uint2*>(ys + sp * (G::PRB * G::COUT * G::PW) + e);
+            // window j's dword = (v_j at sub-column 0, v_j at sub-column 1): low halves of
+            // (u & m0, u & m1) for even j, high halves for odd j
+            const uint32_t a0 = u.x & m0a, b0 = u.x & m1a, a1 = u.y & m0b, b1 = u.y & m1b;
+            bv[sp][nt] = u32x4{__builtin_amdgcn_perm(b0, a0, 0x05040100u), __builtin_amdgcn_perm(b0, a0, 0x07060302u),
+                               __builtin_amdgcn_perm(b1, a1, 0x05040100u), __builtin_amdgcn_perm(b1, a1, 0x07060302u)};
+          }
+          continue;
+        }
         uint32_t mk[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
