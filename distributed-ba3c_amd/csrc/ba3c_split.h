@@ -567,9 +567,15 @@ template <int NS>
 __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, int gx, uint4* lds, uint32_t* red4) {
   using G = Conv0W<NS>;
   using SP = SplitP<NS>;
-  uint16_t* ys = reinterpret_cast<uint16_t*>(lds);
-  uint16_t* xs = ys + G::Y_16;
-  uint8_t* yc8 = reinterpret_cast<uint8_t*>(xs + G::X_16);
+#ifndef BA3C_C0W_XFIRST
+#define BA3C_C0W_XFIRST 1
+#endif
+  // X first: its A-fragment addresses are then lane offset + k-step offset with no LDS base to
+  // add (the base of a region past 1 KB does not fit the ds_read2 offset fields, and the
+  // compiler added it to each of the 14 dword-pair reads of a k-step)
+  uint16_t* xs = reinterpret_cast<uint16_t*>(lds) + (BA3C_C0W_XFIRST ? 0 : G::Y_16);
+  uint16_t* ys = reinterpret_cast<uint16_t*>(lds) + (BA3C_C0W_XFIRST ? G::X_16 : 0);
+  uint8_t* yc8 = reinterpret_cast<uint8_t*>(reinterpret_cast<uint16_t*>(lds) + G::X_16 + G::Y_16);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lq = lane >> 4;
   const int nbands = a.batch * G::NBANDS;
