@@ -328,9 +328,13 @@ struct Band6Ops {
 #pragma unroll
       for (int j = 0; j < MCH; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+#ifndef BA3C_B6_PRIO
+#define BA3C_B6_PRIO 0        // A/B: the MFMA main loop at wave priority 1 (staging at 0)
+#endif
 #pragma unroll 1
       for (int ph = 0; ph < L::NPH; ++ph) {
         if constexpr (L::NPH > 1) stage_phase(ph);
+        if (BA3C_B6_PRIO) __builtin_amdgcn_s_setprio(1);
         const uint16_t* wph = wrow + kfrag(ph * L::KPH);
         constexpr int LA = 3;
         uint4 bring[LA + 1][L::NS];
@@ -409,6 +413,7 @@ struct Band6Ops {
             mfmas();
           }
         }
+        if (BA3C_B6_PRIO) __builtin_amdgcn_s_setprio(0);
       }
 
       // ---- epilogue (16x16 C layout: lane holds column li, rows 4 lq + r) ----

@@ -25,7 +25,7 @@ hipError_t launch_conv0s_fwd(dim3 grid, hipStream_t s, const Conv0SArgs& a) {
 // its plain kernel with (bx, gx) = (block - first block of its job, job grid).
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 wgrad01_pair_kernel(const Wg6Args a1, const Conv0WArgs a0, int g1, int g0) {
-  constexpr int B1 = Conv1W6W::X_BYTES + Conv1W6W::Y_BYTES, B0 = Conv0W<2>::ALLOC_U4 * 16;
+  constexpr int B1 = wgrad6w_lds_bytes<Conv1W6W>(), B0 = Conv0W<2>::ALLOC_U4 * 16;
   __shared__ uint4 lds[(B1 > B0 ? B1 : B0) / 16];
   __shared__ uint32_t red4[4];
   const int b = blockIdx.x;

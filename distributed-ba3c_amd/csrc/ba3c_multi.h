@@ -47,7 +47,7 @@ struct Band6RJob {
 template <class G>
 struct Wg6WJob {
   using Args = Wg6Args;
-  static constexpr int LDS = G::X_BYTES + G::Y_BYTES;
+  static constexpr int LDS = wgrad6w_lds_bytes<G>();
   __device__ static void run(const Args& a, int x, int, int, int gx, char* lds, uint32_t* red4) {
     wgrad6w_body<G>(a, x, gx, lds, red4);
   }

@@ -339,6 +339,15 @@ struct Wg6WGeom {
   static_assert(PX >= NS * XSB && PY >= NS * YSB && PX % 32 == 0 && PY % 32 == 0, "pitches");
   static_assert(RB * WS * (CIN / 4) % 256 == 0, "new X rows: whole float4 per thread");
   static_assert(X_BYTES % 16 == 0 && (HALO * WS * PX) % 16 == 0, "wgrad6w geometry");
+  // 2:4-sparse layout (wgrad6s_units): K = quads of 4 consecutive output pixels of one row (two
+  // pooling windows), QPR per row, 16 quads per k-step of v_smfmac_f32_16x16x64_f16; the pooled
+  // dY as one masked (window 2p, window 2p + 1) dword per (plane, o, quad) and one index nibble
+  // per (o, quad)
+  static constexpr int QPR = WO / 4, NQ = RB * QPR, SKS = (NQ + 15) / 16, NQPAD = 16 * SKS;
+  static constexpr int QS = NQPAD + 4;                     // dwords per (plane, o) row
+  static constexpr int SYQ_BYTES = 2 * COUT * QS * 4, SYI_BYTES = (COUT * QS + 15) / 16 * 16;
+  static constexpr int S_BYTES = X_BYTES + SYQ_BYTES + SYI_BYTES;
+  static_assert(WO % 4 == 0 && COUT == 32 && CIN == 32, "sparse layout: whole quads per row");
 };
 
 // conv1's whole-channel weight-gradient geometry (ba3c_capi.hip Lay<2>::W1W, ba3c_conv0.hip)
@@ -628,9 +637,14 @@ __device__ __forceinline__ void wgrad6w_units(const Wg6Args& a, int bx, int gx, 
           for (int sp = 0; sp < G::NS; ++sp) avb[j][sp] = t[j][sp];
       }
     };
+#ifndef BA3C_W6W_PRIO
+#define BA3C_W6W_PRIO 0       // A/B: the k-steps at wave priority 1 (the staging at 0)
+#endif
+    if (BA3C_W6W_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll 1
     for (int s = 0; s + 1 < G::KS; ++s) kstep(s, std::true_type{});
     kstep(G::KS - 1, std::false_type{});
+    if (BA3C_W6W_PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
   // ---- epilogue: one full slab per workgroup (lane: column o = 16 nb + (lane & 15), rows
@@ -652,21 +666,300 @@ __device__ __forceinline__ void wgrad6w_units(const Wg6Args& a, int bx, int gx, 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 2:4-sparse conv1 weight gradient (BA3C_W6W_SPARSE=1, default).  The un-pooled output
+// gradient dY = MaxPoolGrad(dP) * ReluGrad has at most ONE non-zero per 2x2 window and channel,
+// so along a row of output pixels every group of 4 consecutive pixels (two windows) holds at
+// most 2 non-zeros per channel: exactly the 2:4 structured sparsity of gfx950's
+// v_smfmac_f32_16x16x64_f16, whose sparse A operand covers 64 K values in the issue time of the
+// dense 16x16x32 MFMA (scripts/probes/smfmac_probe.hip: layout, index encoding and rate).  The
+// GEMM is transposed to put dY on that side: dW^T[o][(tap, c)] = sum_p dY[p][o] X[p + tap][c]
+// with M = o (2 m-tiles), N = (tap, 16-channel block) units, K = pixels in quads.
+//  * A (dY^T): lane l = row o = l & 15 (+ 16 m), quads 4 (l >> 4) .. + 3 of the k-step, two
+//    values per quad — window 2p's and 2p+1's gradient where the window's argmax lies in this
+//    pixel row (else 0) — and a nibble per quad: the two positions (argmax column in window 0:
+//    0 / 1, in window 1: 2 / 3).  Staged once per band from the POOLED dP (no un-pooling).
+//  * B (X): lane l = channel l & 15 of the unit, K = quads 2g, 2g + 1, 8 + 2g, 9 + 2g (g = l >>
+//    4) of the k-step: four ds_read_b64_tr_b16 of 4 pixels each per plane.
+// Same products (dY_hi X_hi, dY_hi X_lo, dY_lo X_hi), same scales, same slabs; the k-order
+// differs from the dense body, so the sums agree to rounding, not bit for bit.
+// ---------------------------------------------------------------------------------------
+#ifndef BA3C_W6W_SPARSE
+#define BA3C_W6W_SPARSE 1
+#endif
+#ifndef BA3C_DIAG_W6S
+#define BA3C_DIAG_W6S 0       // diagnostics only (A/B timing): 1 = no band staging, 2 = no MFMA loop
+#endif
+typedef _Float16 f16x16v __attribute__((ext_vector_type(16)));
+
+template <class G, int U0, int NU>
+__device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
+  using SP = SplitP<2>;
+  const int kx = amax_exp(amax_all(a.amax_x, a.batch, red4));
+  const int ky = amax_exp(amax_all(a.amax_dp, a.batch, red4));
+  const float xsc = exp2i(kx), ysc = exp2i(ky);
+  char* yq = xs + G::X_BYTES;                              // [plane][o][QS] dwords
+  uint8_t* yi = reinterpret_cast<uint8_t*>(yq + G::SYQ_BYTES);   // [o][QS] index nibbles
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3, li = lane & 15;
+
+  f32x4 acc[NU][2];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int XQ = G::CIN / 4;
+  constexpr int XPT = G::RB * G::WS * XQ / 256;
+  // dY items of a band: (pooled row, window pair p, o), o fastest (coalesced dP loads)
+  constexpr int YN = (G::RB / 2) * G::QPR * G::COUT;
+  constexpr int YPT = (YN + 255) / 256;
+  float4 xv[XPT];
+  float yv[YPT][2];
+  uint32_t yc[YPT];
+
+  const int ipw = (a.batch + gx - 1) / gx;
+  const int img0 = min(a.batch, bx * ipw), img1 = min(a.batch, img0 + ipw);
+  const int band_end = img1 * G::NBANDS;
+
+  auto load_x = [&](int img, int y, float4 (&v)[XPT]) {
+    const float* src = a.x + ((size_t)(img * G::HS + y) * G::WS) * G::CIN;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) v[i] = reinterpret_cast<const float4*>(src)[tid + 256 * i];
+  };
+  auto load_y = [&](int img, int bi) {
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + 256 * i;
+      const int o = f % G::COUT, rest = f / G::COUT;
+      const int p = rest % G::QPR, pr = bi * (G::RB / 2) + rest / G::QPR;
+      // unconditional loads (past YN: element 0 again, never stored): a load in a branch made
+      // the compiler wait for every outstanding load at the join
+      const size_t e = f < YN ? ((size_t)(img * G::PH + pr) * G::PW + 2 * p) * G::COUT + o : 0;
+      yv[i][0] = a.dp[e];
+      yv[i][1] = a.dp[e + G::COUT];
+      yc[i] = (uint32_t)a.code[e] | ((uint32_t)a.code[e + G::COUT] << 8);
+    }
+  };
+  auto store_x = [&](int wr, const float4 (&v)[XPT]) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int f = tid + 256 * i;
+      const int pix = f / XQ, cq = f - pix * XQ;
+      uint32_t s0[2], s1[2];
+      SP::split(v[i].x, v[i].y, xsc, s0);
+      SP::split(v[i].z, v[i].w, xsc, s1);
+      char* p = xs + (wr * G::WS + pix) * G::PX + cq * 8;
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) *reinterpret_cast<uint2*>(p + sp * G::XSB) = make_uint2(s0[sp], s1[sp]);
+    }
+  };
+  // the band's quads: (pixel row y = 2 pr' + dy, pair p) -> masked dwords + nibbles
+  auto store_y = [&]() {
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int f = tid + 256 * i;
+      if (f < YN) {
+        const int o = f % G::COUT, rest = f / G::COUT;
+        const int p = rest % G::QPR, prl = rest / G::QPR;     // pooled row within the band
+        uint32_t h[2];                                       // (hi, lo) of window 2p / 2p+1
+        {
+          uint32_t s0[2];
+          SP::split(yv[i][0], yv[i][1], ysc, s0);
+          h[0] = s0[0];
+          h[1] = s0[1];
+        }
+        const uint32_t c0 = yc[i] & 255u, c1 = yc[i] >> 8;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+          const bool m0 = c0 != 255u && (c0 >> 1) == (uint32_t)dy;
+          const bool m1 = c1 != 255u && (c1 >> 1) == (uint32_t)dy;
+          const uint32_t mk = (m0 ? 0x0000FFFFu : 0u) | (m1 ? 0xFFFF0000u : 0u);
+          const int Q = (2 * prl + dy) * G::QPR + p;
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp)
+            reinterpret_cast<uint32_t*>(yq)[(sp * G::COUT + o) * G::QS + Q] = h[sp] & mk;
+          yi[o * G::QS + Q] = (uint8_t)((m0 ? (c0 & 1u) : 0u) | ((2u + (m1 ? (c1 & 1u) : 0u)) << 2));
+        }
+      }
+    }
+  };
+
+  // padding quads NQ .. NQPAD - 1: zero values, positions (0, 2); written once
+  for (int i = tid; i < 2 * G::COUT * (G::NQPAD - G::NQ); i += 256) {
+    const int row = i / (G::NQPAD - G::NQ), Q = G::NQ + i % (G::NQPAD - G::NQ);
+    reinterpret_cast<uint32_t*>(yq)[row * G::QS + Q] = 0u;
+    if (row < G::COUT) yi[row * G::QS + Q] = (uint8_t)(2u << 2);
+  }
+  int band = img0 * G::NBANDS;
+  if (band < band_end) {
+    load_x(img0, G::HALO, xv);
+    load_y(img0, 0);
+  }
+  for (; band < band_end; ++band) {
+    const int img = band / G::NBANDS;
+    const int bi = band - img * G::NBANDS;
+    __syncthreads();                                      // previous band's LDS reads are done
+    if (BA3C_DIAG_W6S != 1 && bi > 0) {
+      constexpr int N16 = G::HALO * G::WS * G::PX / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(xs + G::RB * G::WS * G::PX);
+      uint4* dst = reinterpret_cast<uint4*>(xs);
+      for (int i = tid; i < N16; i += 256) dst[i] = src[i];
+      __syncthreads();
+    }
+    if (BA3C_DIAG_W6S != 1) {
+      store_x(G::HALO, xv);
+      store_y();
+      if (bi == 0) {
+        load_x(img, 0, xv);
+        store_x(0, xv);
+      }
+    }
+    __syncthreads();
+    if (BA3C_DIAG_W6S != 1 && band + 1 < band_end) {
+      const int ni = (band + 1) / G::NBANDS, nbi = band + 1 - ni * G::NBANDS;
+      load_x(ni, nbi * G::RB + G::HALO, xv);
+      load_y(ni, nbi);
+    }
+    if (BA3C_DIAG_W6S == 2) continue;
+
+    // per k-step: the lane's four quad pixel bases (B reads) and its A / index words
+    int xq[4];
+    auto addr = [&](int s, int (&xo)[4]) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int Q = 16 * s + (r >> 1) * 8 + 2 * g + (r & 1);
+        const int y = Q < G::NQ ? Q / G::QPR : 0, p = Q < G::NQ ? Q - (Q / G::QPR) * G::QPR : 0;
+        xo[r] = (y * G::WS + 4 * p + q) * G::PX + 8 * pq;
+      }
+    };
+    auto read_a = [&](int s, u32x4 (&av)[2][2], uint32_t (&ix)[2]) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int o = 16 * m + li;
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const uint4 u = *reinterpret_cast<const uint4*>(yq + ((sp * G::COUT + o) * G::QS + 16 * s + 4 * g) * 4);
+          av[m][sp] = u32x4{u.x, u.y, u.z, u.w};
+        }
+        const uint32_t b = *reinterpret_cast<const uint32_t*>(yi + o * G::QS + 16 * s + 4 * g);
+        const uint32_t t = (b | (b >> 4)) & 0x00FF00FFu;     // nibbles of quads 0..3 -> 16 bits
+        ix[m] = (t | (t >> 8)) & 0xFFFFu;
+      }
+    };
+    auto read_b = [&](int u, const int (&xo)[4], u32x4 (&bv)[2][2]) {
+      const int unit = U0 + u, tap = unit / G::CB, cb = unit - tap * G::CB;
+      const int kh = tap / G::KW, kw = tap - kh * G::KW;
+      const int off = (kh * G::WS + kw) * G::PX + cb * 32;    // compile-time
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        const uint2 r0 = lds_tr16(xs + xo[0] + off + sp * G::XSB);
+        const uint2 r1 = lds_tr16(xs + xo[1] + off + sp * G::XSB);
+        const uint2 r2 = lds_tr16(xs + xo[2] + off + sp * G::XSB);
+        const uint2 r3 = lds_tr16(xs + xo[3] + off + sp * G::XSB);
+        bv[sp][0] = u32x4{r0.x, r0.y, r1.x, r1.y};
+        bv[sp][1] = u32x4{r2.x, r2.y, r3.x, r3.y};
+      }
+    };
+    u32x4 av[2][2], avn[2][2];
+    uint32_t ix[2], ixn[2];
+    u32x4 bb[2][2][2];                                    // [buffer][plane][half]
+    addr(0, xq);
+    read_a(0, av, ix);
+    read_b(0, xq, bb[0]);
+    auto kstep = [&](int s, auto pf) {
+      constexpr bool PF = decltype(pf)::value;
+      int xn[4];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        if (u + 1 < NU) {
+          read_b(u + 1, xq, bb[(u + 1) & 1]);
+        } else if (PF) {
+          addr(s + 1, xn);
+          read_a(s + 1, avn, ixn);
+          read_b(0, xn, bb[NU & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);                // keep those reads ahead of the MFMAs
+        const u32x4 (&bu)[2][2] = bb[u & 1];
+        f16x16v b16[2];
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const u32x4 lo = bu[sp][0], hi = bu[sp][1];
+          typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+          const u32x8 w = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          b16[sp] = __builtin_bit_cast(f16x16v, w);
+        }
+        // dY_hi X_hi, dY_hi X_lo, dY_lo X_hi (SplitP<2>'s products, dY on the sparse side)
+#pragma unroll
+        for (int pr = 0; pr < 3; ++pr)
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+            acc[u][m] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(
+                __builtin_bit_cast(f16x8, av[m][pr == 2 ? 1 : 0]), b16[pr == 1 ? 1 : 0], acc[u][m], (int)ix[m], 0, 0);
+      }
+      if (PF) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          av[m][0] = avn[m][0];
+          av[m][1] = avn[m][1];
+          ix[m] = ixn[m];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xq[r] = xn[r];
+        if (NU & 1) {                                     // the next step's unit 0 is in bb[1]
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp) {
+            bb[0][sp][0] = bb[1][sp][0];
+            bb[0][sp][1] = bb[1][sp][1];
+          }
+        }
+      }
+    };
+#pragma unroll 1
+    for (int s = 0; s + 1 < G::SKS; ++s) kstep(s, std::true_type{});
+    kstep(G::SKS - 1, std::false_type{});
+  }
+
+  // ---- epilogue: C 16x16: lane holds column li = channel 16 cb + li, rows o = 16 m + 4 g + r
+  float* pz = a.part + (size_t)bx * G::M * G::COUT;
+  const float us1 = exp2i(-kx), us2 = exp2i(-ky);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int unit = U0 + u, tap = unit / G::CB, cb = unit - tap * G::CB;
+    const int c = 16 * cb + li;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = 16 * m + 4 * g + r;
+        pz[((size_t)tap * G::CIN + c) * G::COUT + o] = acc[u][m][r] * us1 * us2;
+      }
+  }
+}
+
 template <class G>
 __device__ __forceinline__ void wgrad6w_body(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
   using U = Wg6WUnits<G>;
   static_assert(U::u0(4) == U::UNITS && U::nu(0) <= U::MAXU, "unit partition");
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgrad6w_units<G, U::u0(0), U::nu(0)>(a, bx, gx, xs, red4); break;
-    case 1: wgrad6w_units<G, U::u0(1), U::nu(1)>(a, bx, gx, xs, red4); break;
-    case 2: wgrad6w_units<G, U::u0(2), U::nu(2)>(a, bx, gx, xs, red4); break;
-    default: wgrad6w_units<G, U::u0(3), U::nu(3)>(a, bx, gx, xs, red4); break;
+#define BA3C_W6W_CASE(w)                                                                  \
+    if constexpr (BA3C_W6W_SPARSE) wgrad6s_units<G, U::u0(w), U::nu(w)>(a, bx, gx, xs, red4); \
+    else wgrad6w_units<G, U::u0(w), U::nu(w)>(a, bx, gx, xs, red4);
+    case 0: BA3C_W6W_CASE(0) break;
+    case 1: BA3C_W6W_CASE(1) break;
+    case 2: BA3C_W6W_CASE(2) break;
+    default: BA3C_W6W_CASE(3) break;
+#undef BA3C_W6W_CASE
   }
+}
+
+// LDS bytes of wgrad6w_body (dense: X window + un-pooled dY; sparse: X window + quads)
+template <class G>
+__host__ __device__ constexpr int wgrad6w_lds_bytes() {
+  return BA3C_W6W_SPARSE ? G::S_BYTES : G::X_BYTES + G::Y_BYTES;
 }
 
 template <class G>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wgrad6w_kernel(const Wg6Args a) {
-  __shared__ uint4 lds4[(G::X_BYTES + G::Y_BYTES) / 16];
+  __shared__ uint4 lds4[wgrad6w_lds_bytes<G>() / 16];
   __shared__ uint32_t red4[4];
   wgrad6w_body<G>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4), red4);
 }
