@@ -329,7 +329,7 @@ struct Band6Ops {
       for (int j = 0; j < MCH; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #ifndef BA3C_B6_PRIO
-#define BA3C_B6_PRIO 0        // A/B: the MFMA main loop at wave priority 1 (staging at 0)
+#define BA3C_B6_PRIO 1        // the MFMA main loop at wave priority 1, the staging at 0 (r05 A/B: conv1 fwd -1 %, dgrad -2 %)
 #endif
 #pragma unroll 1
       for (int ph = 0; ph < L::NPH; ++ph) {

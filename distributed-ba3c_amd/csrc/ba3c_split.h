@@ -563,10 +563,14 @@ __device__ __forceinline__ uint32_t c0w_mask16_eq0(uint32_t d) {
 
 // bx / gx: first band and persistent stride (blockIdx.x / gridDim.x of the plain kernel; a
 // paired launch passes its own); lds: Conv0W<NS>::ALLOC_U4 uint4 of LDS, red4: 4 words
+#ifndef BA3C_C0W_SPARSE
+#define BA3C_C0W_SPARSE 1
+#endif
 template <int NS>
 __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, int gx, uint4* lds, uint32_t* red4) {
   using G = Conv0W<NS>;
   using SP = SplitP<NS>;
+  constexpr bool C0W_SPARSE = BA3C_C0W_SPARSE && NS == 2;
 #ifndef BA3C_C0W_XFIRST
 #define BA3C_C0W_XFIRST 1
 #endif
@@ -672,6 +676,36 @@ __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, i
       // B: un-pool 4 windows (pooled cols x0/2 .. +3 of pooled row r/2) for channel o
       const uint32_t sy = (uint32_t)(r & 1);
       const int e0 = ((r >> 1) * G::COUT + li) * G::PW + (x0 >> 1);
+      if constexpr (C0W_SPARSE) {
+        // 2:4-sparse form (BA3C_C0W_SPARSE): dY^T on the sparse A side of
+        // v_smfmac_f32_16x16x32_f16 (rows o, the lane's 8 pixels = 2 quads of 2 windows each),
+        // the frames' fragments above as its dense B (columns (tap, c)).  Per quad the two kept
+        // values are the windows' gradients where their argmax lies in this pixel row (else 0)
+        // at positions (argmax column) and (2 + argmax column): no un-pooling at all.
+        const uint32_t sx = sy * 0x00020002u;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int e = e0 + 16 * m * G::PW;
+          const uint32_t cw = *reinterpret_cast<const uint32_t*>(yc8 + e);
+          // (code ^ 2 sy) & ~1 == 0 <=> the argmax is in this pixel row (255 never is)
+          const uint32_t m01 = c0w_mask16_eq0((__builtin_amdgcn_perm(cw, cw, 0x0C010C00u) ^ sx) & 0x00FE00FEu);
+          const uint32_t m23 = c0w_mask16_eq0((__builtin_amdgcn_perm(cw, cw, 0x0C030C02u) ^ sx) & 0x00FE00FEu);
+          // index nibbles: quad 0 = (c0 & 1) | (2 + (c1 & 1)) << 2, quad 1 from c2, c3
+          const uint32_t t = cw & 0x01010101u;
+          const uint32_t t1 = t | (t >> 6);
+          const int ix = (int)(((t1 | (t1 >> 12)) & 0x55u) | 0x88u);
+#pragma unroll
+          for (int sp = 0; sp < NS; ++sp) {
+            const uint2 u = *reinterpret_cast<const uint2*>(ys + sp * (G::PRB * G::COUT * G::PW) + e);
+            typedef _Float16 f16x4c __attribute__((ext_vector_type(4)));
+            const f16x4c av4 = __builtin_bit_cast(f16x4c, make_uint2(u.x & m01, u.y & m23));
+#pragma unroll
+            for (int mt = 0; mt < G::MT; ++mt)
+              acc[mt][m] = __builtin_amdgcn_smfmac_f32_16x16x32_f16(av4, __builtin_bit_cast(f16x8, av[mt]), acc[mt][m], ix, 0, 0);
+          }
+        }
+        continue;
+      }
       u32x4 bv[NS][2];
 #ifndef BA3C_C0W_PKMASK
 #define BA3C_C0W_PKMASK 1
@@ -728,7 +762,8 @@ __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, i
   }
 
   // ---- epilogue: the four waves' accumulators go through LDS and are summed in wave order
-  // into ONE slab per workgroup (lane holds rows 16 mt + 4 lq + r, column 16 nt + li) ----
+  // into ONE slab per workgroup (dense: lane holds rows (tap, c) 16 mt + 4 lq + r, column
+  // o = 16 nt + li; sparse: rows o = 16 m + 4 lq + r, column (tap, c) = 16 mt + li) ----
   static_assert(4 * G::M * G::COUT * 4 <= G::ALLOC_U4 * 16, "slab staging fits the band LDS");
   float* red = reinterpret_cast<float*>(lds);
   __syncthreads();                                     // last band's LDS reads are done
@@ -738,8 +773,13 @@ __device__ __forceinline__ void conv0s_wgrad_body(const Conv0WArgs& a, int bx, i
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int tap = C0W_TAP_OUT[4 * mt + lq];        // row 4 lq + r = (slot lq, channel r)
-        if (tap >= 0) red[(wave * G::M + tap * G::C + r) * G::COUT + 16 * nt + li] = acc[mt][nt][r];
+        if constexpr (C0W_SPARSE) {
+          const int tap = C0W_TAP_OUT[4 * mt + (li >> 2)], c = li & 3, o = 16 * nt + 4 * lq + r;
+          if (tap >= 0) red[(wave * G::M + tap * G::C + c) * G::COUT + o] = acc[mt][nt][r];
+        } else {
+          const int tap = C0W_TAP_OUT[4 * mt + lq];      // row 4 lq + r = (slot lq, channel r)
+          if (tap >= 0) red[(wave * G::M + tap * G::C + r) * G::COUT + 16 * nt + li] = acc[mt][nt][r];
+        }
       }
   __syncthreads();
   float* pz = a.part + (size_t)bx * G::M * G::COUT;

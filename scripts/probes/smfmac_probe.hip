@@ -19,6 +19,31 @@ __global__ void one(const f16x8* a, const f16x16* b, const int* idx, f32x4* c) {
   c[l] = acc;
 }
 
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+__global__ void one32(const f16x4* a, const f16x8* b, const int* idx, f32x4* c) {
+  const int l = threadIdx.x;
+  f32x4 acc = {0, 0, 0, 0};
+  acc = __builtin_amdgcn_smfmac_f32_16x16x32_f16(a[l], b[l], acc, idx[l], 0, 0);
+  c[l] = acc;
+}
+__global__ void rate32(const f16x8* a, const f16x16* b, const int* idx, f32x4* c, int iters) {
+  const int l = threadIdx.x & 63;
+  f16x8 a8 = a[l];
+  f16x4 av = {a8[0], a8[1], a8[2], a8[3]};
+  f16x16 bv = b[l];
+  f16x8 bl = {bv[0], bv[1], bv[2], bv[3], bv[4], bv[5], bv[6], bv[7]};
+  const int ix = idx[l];
+  f32x4 acc[8];
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0, 0, 0, 0};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = __builtin_amdgcn_smfmac_f32_16x16x32_f16(av, bl, acc[j], ix, 0, 0);
+  }
+  f32x4 s = acc[0];
+  for (int j = 1; j < 8; ++j) s += acc[j];
+  c[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <bool SPARSE>
 __global__ void rate(const f16x8* a, const f16x16* b, const int* idx, f32x4* c, int iters) {
   const int l = threadIdx.x & 63;
@@ -106,6 +131,50 @@ int main() {
           }
         printf("A-layout %d B-layout %d index %d: mismatches %d (transposed C: %d)\n", ha, hb, hi, bad, badT);
       }
+  // v_smfmac_f32_16x16x32_f16 (A 16 x 32 logical, 4 stored halves per lane; B 32 x 16): lane
+  // layouts 0 / 1 for the A and B halves of K (16 lanes per K block of 8), nibble order 0 / 1
+  for (int hb = 0; hb < 2; ++hb)
+    for (int hi = 0; hi < 2; ++hi) {
+      std::vector<_Float16> a(64 * 4); std::vector<_Float16> b(64 * 8); std::vector<int> ix(64, 0);
+      for (int l = 0; l < 64; ++l) {
+        const int r = l & 15, g = l >> 4;
+        int bits = 0;
+        for (int q = 0; q < 2; ++q) {
+          const int k0 = 8 * g + 4 * q;
+          int pos[2], np = 0;
+          for (int j = 0; j < 4 && np < 2; ++j) if (A[r][k0 + j] != 0.f) pos[np++] = j;
+          while (np < 2) { pos[np] = (np == 0 ? 0 : (pos[0] == 3 ? 2 : 3)); if (np == 1 && pos[1] < pos[0]) { int t = pos[0]; pos[0] = pos[1]; pos[1] = t; } ++np; }
+          a[4 * l + 2 * q] = (_Float16)A[r][k0 + pos[0]];
+          a[4 * l + 2 * q + 1] = (_Float16)A[r][k0 + pos[1]];
+          const int nib = hi == 0 ? (pos[0] | (pos[1] << 2)) : (pos[1] | (pos[0] << 2));
+          bits |= nib << (4 * q);
+        }
+        ix[l] = bits;
+        const int n = l & 15;
+        for (int e = 0; e < 8; ++e) {
+          const int k = hb == 0 ? 8 * g + e : (e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4));
+          b[8 * l + e] = (_Float16)B[k][n];
+        }
+      }
+      // reference over K 0..31 only
+      float C32[16][16];
+      for (int r = 0; r < 16; ++r)
+        for (int n = 0; n < 16; ++n) {
+          float s = 0;
+          for (int k = 0; k < 32; ++k) s += A[r][k] * B[k][n];
+          C32[r][n] = s;
+        }
+      hipMemcpy(da, a.data(), 64 * 8, hipMemcpyHostToDevice);
+      hipMemcpy(db, b.data(), 64 * 16, hipMemcpyHostToDevice);
+      hipMemcpy(di, ix.data(), 64 * 4, hipMemcpyHostToDevice);
+      one32<<<1, 64>>>(reinterpret_cast<const f16x4*>(da), reinterpret_cast<const f16x8*>(db), di, dc);
+      std::vector<f32x4> c(64);
+      hipMemcpy(c.data(), dc, 64 * sizeof(f32x4), hipMemcpyDeviceToHost);
+      int bad = 0;
+      for (int l = 0; l < 64; ++l)
+        for (int i = 0; i < 4; ++i) bad += fabsf(c[l][i] - C32[4 * (l >> 4) + i][l & 15]) > 1e-3f;
+      printf("16x16x32: B-layout %d index %d: mismatches %d\n", hb, hi, bad);
+    }
   // issue rate: 2048 workgroups x 256 threads, 8 independent accumulators per wave
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const int iters = 4096;
@@ -122,5 +191,14 @@ int main() {
              sp ? "smfmac_16x16x64_f16" : "mfma_16x16x32_f16", ms, flop / ms / 1e9,
              ms * 1e6 / (n / 1024.0));
     }
+  for (int rep = 0; rep < 2; ++rep) {
+    hipEventRecord(e0);
+    rate32<<<2048, 256>>>(da, db, di, dc, iters);
+    hipEventRecord(e1); hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    const double n = 2048.0 * 4 * iters * 8;
+    printf("smfmac_16x16x32_f16: %.3f ms, %.1f logical TFLOP/s, %.2f ns per wave-instruction per SIMD\n", ms,
+           n * 16.0 * 16 * 32 * 2 / ms / 1e9, ms * 1e6 / (n / 1024.0));
+  }
   return 0;
 }
