@@ -692,6 +692,13 @@ __device__ __forceinline__ void wgrad6w_units(const Wg6Args& a, int bx, int gx, 
 #endif
 typedef _Float16 f16x16v __attribute__((ext_vector_type(16)));
 
+// Logical quad J (the MFMA's K / 4) -> physical quad of the k-step: bits 0 and 1 swapped
+// within each group of 4 (an involution).  A 32-lane half of a B read (ds_read_b64_tr_b16)
+// holds lane groups g and g + 1, whose quads are J and J + 2: in physical order they are
+// neighbours, 4 pixels = 4 x 40 dwords apart = the other 32 banks (row order put them 8 pixels
+// = 320 dwords apart: the same banks, a 2-way conflict on every B read, PMC r05i).
+__device__ __forceinline__ constexpr int s_pi(int j) { return (j & ~3) | ((j & 1) << 1) | ((j >> 1) & 1); }
+
 template <class G, int U0, int NU>
 __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, char* xs, uint32_t* red4) {
   using SP = SplitP<2>;
@@ -773,7 +780,8 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
           const bool m0 = c0 != 255u && (c0 >> 1) == (uint32_t)dy;
           const bool m1 = c1 != 255u && (c1 >> 1) == (uint32_t)dy;
           const uint32_t mk = (m0 ? 0x0000FFFFu : 0u) | (m1 ? 0xFFFF0000u : 0u);
-          const int Q = (2 * prl + dy) * G::QPR + p;
+          const int Qp = (2 * prl + dy) * G::QPR + p;     // physical quad -> logical slot
+          const int Q = (Qp & ~15) | s_pi(Qp & 15);
 #pragma unroll
           for (int sp = 0; sp < 2; ++sp)
             reinterpret_cast<uint32_t*>(yq)[(sp * G::COUT + o) * G::QS + Q] = h[sp] & mk;
@@ -826,7 +834,8 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
     auto addr = [&](int s, int (&xo)[4]) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int Q = 16 * s + (r >> 1) * 8 + 2 * g + (r & 1);
+        // logical quad J of the read; its pixels sit in physical quad s_pi(J) (see below)
+        const int Q = 16 * s + s_pi((r >> 1) * 8 + 2 * g + (r & 1));
         const int y = Q < G::NQ ? Q / G::QPR : 0, p = Q < G::NQ ? Q - (Q / G::QPR) * G::QPR : 0;
         xo[r] = (y * G::WS + 4 * p + q) * G::PX + 8 * pq;
       }
