@@ -95,8 +95,11 @@ class Ba3cTrainer(object):
         if flags & 2:
             what.append("bit 1: a one-launch bucket clip (ba3c_clip_grads_range) gave up waiting, "
                         "so invalid clipped gradients entered the all-reduce")
-        if flags & ~3:
-            what.append("unknown bits 0x%x" % (flags & ~3))
+        if flags & 4:
+            what.append("bit 2: a chained launch's waiting workgroups gave up waiting for their "
+                        "producers (rerun with BA3C_CHAIN=0)")
+        if flags & ~7:
+            what.append("unknown bits 0x%x" % (flags & ~7))
         return "; ".join(what)
 
     def check_device_errors(self):

@@ -719,6 +719,7 @@ struct WPrep6Args {
   uint32_t* amax;          // max-|x| slots zeroed here (n_amax words; may be null)
   int n_amax;
   int* wexp;               // [8]: weight scale exponents of jobs 0..5 and conv0 (slot 7)
+  int coherent;            // 1: zero with agent-scope stores (read inside the same chained launch)
 };
 
 // (bx, by, gx): blockIdx.x, blockIdx.y, gridDim.x of a plain launch; red4: 4 floats of LDS
@@ -726,11 +727,18 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
   const int y = by;
   if (y == 0) {
     if (a.relu)
-      for (int i = bx * 256 + threadIdx.x; i < RELU_WORDS; i += gx * 256) a.relu[i] = 0ull;
+      for (int i = bx * 256 + threadIdx.x; i < RELU_WORDS; i += gx * 256) {
+        if (a.coherent) st_agent_u64(a.relu + i, 0ull);
+        else a.relu[i] = 0ull;
+      }
     if (a.amax)
-      for (int i = bx * 256 + threadIdx.x; i < a.n_amax; i += gx * 256) a.amax[i] = 0u;
+      for (int i = bx * 256 + threadIdx.x; i < a.n_amax; i += gx * 256) {
+        if (a.coherent) st_agent_u32(a.amax + i, 0u);
+        else a.amax[i] = 0u;
+      }
   }
   if (y == a.jobs.njobs) {
+    if (!a.w0) return;                 // zeroing only (conv0 splits its own fragments)
     const int k = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, red4)));
     if (bx == 0 && threadIdx.x == 0) a.wexp[7] = k;
     conv0s_wprep_one(a.w0, a.wb0, bx * 256 + threadIdx.x, k);

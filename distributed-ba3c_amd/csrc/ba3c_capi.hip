@@ -79,6 +79,8 @@ struct TensorDesc {
   int32_t ndim;
 };
 
+constexpr int CHAIN_SITES = 1;   // chained launch sites (launch_chain)
+
 struct ba3c_handle {
   ba3c_config cfg;
   std::vector<TensorDesc> tensors;
@@ -136,6 +138,11 @@ struct ba3c_handle {
   // clip_range_kernel's (a generation space of their own) follow them
   unsigned long long* utag = nullptr;
   unsigned long long* ctag = nullptr;
+  // chained multi-job launches (ba3c_multi.h: an in-launch dependency instead of a kernel
+  // boundary): CHAIN_SITES x 4 words + an error word after the tags (null: no device memory,
+  // unchained launches).  BA3C_CHAIN=0: unchained.
+  bool chain_on = true;
+  unsigned* chain = nullptr;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -461,6 +468,40 @@ int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const type
   return BA3C_OK;
 }
 
+// A chained multi-job launch (ba3c_multi.h): jobs [0, nsig) signal, the jobs in `wmask` wait
+// for them (those in `late` inside their body); `site` picks the launch site's counter words.
+// Callers check chain_ok() first.
+constexpr int CHAIN_PREP_CONV0 = 0;
+bool chain_ok(const ba3c_handle* h) { return h->chain_on && h->chain != nullptr; }
+
+template <bool W2, class J0, class J1, class J2 = NoJob>
+int launch_chain(hipStream_t s, int site, int nsig, int wmask, int late, const typename J0::Args& a0, dim3 g0,
+                 const typename J1::Args& a1, dim3 g1, const typename J2::Args& a2 = typename J2::Args{},
+                 dim3 g2 = dim3(0, 1, 1), ba3c_handle* h = nullptr, int kid = -1) {
+  MultiGrid g;
+  const dim3 gs[3] = {g0, g1, g2};
+  int end = 0;
+  for (int j = 0; j < 3; ++j) {
+    g.gx[j] = (int)gs[j].x;
+    g.gy[j] = (int)gs[j].y;
+    end += (int)(gs[j].x * gs[j].y * gs[j].z);
+    g.end[j] = end;
+  }
+  if (end == 0) return BA3C_OK;
+  int nwait = 0;
+  for (int j = 0; j < 3; ++j)
+    if ((wmask >> j) & 1) nwait += g.end[j] - (j ? g.end[j - 1] : 0);
+  const ChainArgs c{h->chain + 4 * site, h->chain + 4 * CHAIN_SITES, nsig, wmask, nwait, late};
+  std::optional<ProbeScope> probe;
+  if (kid >= 0) probe.emplace(h, s, kid);
+  if constexpr (W2)
+    hipLaunchKernelGGL((multi_chain_kernel_w2<J0, J1, J2>), dim3(end), dim3(256), 0, s, a0, a1, a2, g, c);
+  else
+    hipLaunchKernelGGL((multi_chain_kernel<J0, J1, J2>), dim3(end), dim3(256), 0, s, a0, a1, a2, g, c);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
 // band conv on split MFMA; `ringable`: a multi-band layout that may run as the ring-walk
 // persistent kernel (whole images per workgroup) at large batches
 template <class L>
@@ -554,10 +595,26 @@ int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, con
   rest.w0 = nullptr;                    // rows 0..njobs-1 only, no zeroing: conv0 publishes
   rest.relu = nullptr;                  // into those counters concurrently
   rest.amax = nullptr;
-  hipLaunchKernelGGL(wprep6_kernel, dim3(64, 1), dim3(256), 0, s, first);
-  HIP_TRY(hipGetLastError());
   const Conv0SArgs sa{state, reinterpret_cast<const uint4*>(w.wt + WT_C0S), w.p0, train ? w.c0 : nullptr,
                       train ? w.relu : nullptr, B, w.wexp + WX_CONV0, w.am(AM_P0, h)};
+  const int nconv0 = std::min(FW_P0S, B * Conv0S::NBANDS);
+  if (chain_ok(h) && nconv0 <= h->cus) {
+    // one launch: the zeroing workgroups signal; conv0's forward (at most one workgroup per
+    // CU) splits its own weight fragments and waits for the zeroing before its first
+    // publication; the band-conv weight jobs run beside it
+    first.coherent = 1;
+    first.w0 = nullptr;
+    Conv0SArgs sc = sa;
+    sc.w0 = prm + h->tensors[h->idx_conv[0]].offset;
+    sc.zsig = h->chain + 4 * CHAIN_PREP_CONV0 + 1;
+    sc.zneed = 64;
+    sc.zerr = h->chain + 4 * CHAIN_SITES;
+    return launch_chain<true, WPrep6Job, Conv0SJob, WPrep6Job>(
+        s, CHAIN_PREP_CONV0, 1, 2, 2, first, dim3(64, 1), sc, dim3(nconv0), rest,
+        dim3(64, rest.jobs.njobs), h, BA3C_K_CONV0_FWD);
+  }
+  hipLaunchKernelGGL(wprep6_kernel, dim3(64, 1), dim3(256), 0, s, first);
+  HIP_TRY(hipGetLastError());
   ProbeScope ps(h, s, BA3C_K_CONV0_FWD);
   // two workgroups per CU (the register budget of conv0's plain kernel): without the bound the
   // compiler gave the fused body 216 VGPRs + 52 AGPRs, one wave per SIMD, so at B=32 the 160 conv0
@@ -600,6 +657,10 @@ int launch_conv3(ba3c_handle* h, hipStream_t s, int kid, const Conv3Args& a) {
 }
 
 // ---- forward --------------------------------------------------------------------------
+#ifndef BA3C_FC_DEPTH
+#define BA3C_FC_DEPTH 2       // k-tile ring depth of fc1's forward at full grids (A/B)
+#endif
+
 // Split kernels (h->band): conv0 (C == 4) and the conv1 / conv2 band convolutions on scaled
 // fp16 hi/lo MFMA (ba3c_split.h, ba3c_band6.h); C == 12's conv0, conv3 and fc1 on the bf16x6
 // GEMM engine.  BA3C_GENERIC=1: every layer on the fp32-MFMA GEMM engine.
@@ -671,9 +732,6 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
                          dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, 4>), grid, dim3(GEMM_THREADS), 0, s, fc);
-#ifndef BA3C_FC_DEPTH
-#define BA3C_FC_DEPTH 2       // k-tile ring depth of fc1's forward at full grids (A/B)
-#endif
     else if (h->g6)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, BA3C_FC_DEPTH>), grid, dim3(GEMM_THREADS), 0, s, fc);
     else
@@ -710,7 +768,6 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   const float* W2c = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3c = prm + h->tensors[h->idx_conv[3]].offset;
   const float* Wfc = prm + h->tensors[h->idx_fc1].offset;
-  if (phase != 2) std::memset(h->merged, 0, sizeof(h->merged));   // a new training pass
   bool defer_w1 = false;   // conv1's weight gradient waits for conv0's (one paired launch)
   // The weight-gradient kernels (heads, fc1, conv3..conv1) run on the side stream `ws`,
   // each after the event that publishes its output gradient; the input-gradient chain and
@@ -1133,10 +1190,11 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   };
   static const Switch kSwitches[] = {{"BA3C_GENERIC", 0, 1},  {"BA3C_C1PAIR", 0, 2},   {"BA3C_SCALARS_RIDE", 0, 1},
                                      {"BA3C_OVERLAP", 0, 2},  {"BA3C_MULTI", 0, 1},    {"BA3C_MULTI_BIG", 0, 3},
-                                     {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}};
-  int sw[8];
-  const int defaults[8] = {0, 2, 1, 2, 1, 3, 1, 1};
-  for (int i = 0; i < 8; ++i) {
+                                     {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}, {"BA3C_CHAIN", 0, 1}};
+  constexpr int NSW = 9;
+  int sw[NSW];
+  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1};
+  for (int i = 0; i < NSW; ++i) {
     sw[i] = defaults[i];
     const char* e = getenv(kSwitches[i].name);
     if (!e) continue;
@@ -1155,6 +1213,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   h->multi_big = sw[5];
   h->fused_update = sw[6] != 0;
   h->ring = sw[7] != 0;
+  h->chain_on = sw[8] != 0;
   h->g6 = h->band;
   {
     int dev = 0, n = 0;
@@ -1223,15 +1282,17 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   // clip_update_kernel's and clip_range_kernel's tagged partials + error words (no device:
   // stay null, two-launch paths)
   const size_t ubytes = ((size_t)tt.nchunks + 1) * sizeof(unsigned long long);
-  if (hipMalloc(reinterpret_cast<void**>(&h->utag), 2 * ubytes) != hipSuccess) {
+  const size_t cbytes = (4 * CHAIN_SITES + 4) * sizeof(unsigned);
+  if (hipMalloc(reinterpret_cast<void**>(&h->utag), 2 * ubytes + cbytes) != hipSuccess) {
     h->utag = nullptr;
     (void)hipGetLastError();
-  } else if (hipMemset(h->utag, 0, 2 * ubytes) != hipSuccess) {
+  } else if (hipMemset(h->utag, 0, 2 * ubytes + cbytes) != hipSuccess) {
     (void)hipFree(h->utag);
     h->utag = nullptr;
     (void)hipGetLastError();
   } else {
     h->ctag = h->utag + tt.nchunks + 1;
+    h->chain = reinterpret_cast<unsigned*>(h->ctag + tt.nchunks + 1);
   }
   *out = h;
   return BA3C_OK;
@@ -1305,6 +1366,7 @@ int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
   Workspace w = carve(h, workspace, batch, false);
+  std::memset(h->merged, 0, sizeof(h->merged));
   int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, false)
                                : run_forward<12>(h, s, params, state, batch, w, false);
   if (r != BA3C_OK) return r;
@@ -1351,6 +1413,7 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
   if (phase == 2)   // conv layers' backward on the workspace phase 1 left
     return h->cfg.channels == 4 ? run_backward<4>(h, s, params, state, batch, w, grads, 2)
                                 : run_backward<12>(h, s, params, state, batch, w, grads, 2);
+  std::memset(h->merged, 0, sizeof(h->merged));   // a new training pass
   // on the split path the weight-prep launch zeroes the ReLU counters
   if (!h->band) HIP_TRY(hipMemsetAsync(w.relu, 0, RELU_WORDS * 8, s));
   int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, true)
@@ -1633,10 +1696,11 @@ int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
   if (!h || !flags) return fail(BA3C_ERR_INVALID, "null argument");
   *flags = 0;
   if (!h->utag) return BA3C_OK;
-  uint32_t e = 0, e2 = 0;
+  uint32_t e = 0, e2 = 0, e3 = 0;
   HIP_TRY(hipMemcpy(&e, h->utag + h->table.nchunks, sizeof(e), hipMemcpyDeviceToHost));
   if (h->ctag) HIP_TRY(hipMemcpy(&e2, h->ctag + h->table.nchunks, sizeof(e2), hipMemcpyDeviceToHost));
-  *flags = e | (e2 << 1);
+  if (h->chain) HIP_TRY(hipMemcpy(&e3, h->chain + 4 * CHAIN_SITES, sizeof(e3), hipMemcpyDeviceToHost));
+  *flags = e | (e2 << 1) | (e3 << 2);
   return BA3C_OK;
 }
 

@@ -113,6 +113,81 @@ __device__ __forceinline__ void multi_body(const typename J0::Args& a0, const ty
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Chained multi-job launch: an in-launch dependency instead of a kernel boundary (configs[1],
+// B=32: the zeroing of the step's ReLU counters / max slots -> conv0's forward, which splits
+// its own weight fragments and waits only before its first publication into those words).
+// Jobs [0, nsig) signal when a workgroup is done; the jobs in `wmask` wait until every
+// signalling workgroup has — before their body, or inside it (`late`: the body polls the
+// count itself).  Nothing assumes a dispatch order: signalling workgroups never wait, and the
+// host chains a launch only when its waiting workgroups fit one per CU, so they cannot keep a
+// signalling workgroup from being scheduled.  Hand-off without fences (MI355X_MICROARCH.md
+// §Correctness boundaries, the sc1 form): every handed-off word is stored with an agent-scope
+// store (global_store sc1: it leaves the XCD's non-coherent L2) and used only by device-scope
+// atomics or agent-scope loads; each storing wave drains (s_waitcnt 0), the workgroup
+// barriers, then thread 0 bumps the signal count.  Measured and not kept (r05k-n): a
+// per-workgroup release / acquire (an L2 write-back each: +18 us per B=32 step), a ticket
+// counter drawn by every workgroup (+40 us: same-address returning atomics serialise), fc1's
+// split-K forward chained with the heads over sc1 partials (14.3 -> 16.9 us), conv0 reading
+// the prep's fragments with sc1 loads (21.2 -> 26.4 us).  The last waiting workgroup resets
+// the words (every signal was counted before any waiter passed), so each launch starts from
+// zeros (ba3c_create zeroes them; graph replays included).  Waits are bounded: a broken
+// assumption sets the error word instead of hanging the device.
+struct ChainArgs {
+  unsigned* w;      // [4]: ticket, signals, finished
+  unsigned* err;    // bit 0: a wait gave up (ba3c_device_errors bit 2)
+  int nsig, wmask, nwait;   // nwait: workgroups of the waiting jobs
+  int late;                 // waiting jobs that wait inside their body (not before it)
+};
+
+__device__ __forceinline__ unsigned chain_ld(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class J0, class J1, class J2>
+__device__ __forceinline__ void multi_chain_body(const typename J0::Args& a0, const typename J1::Args& a1,
+                                                 const typename J2::Args& a2, const MultiGrid& g,
+                                                 const ChainArgs& c, char* lds, uint32_t* red4) {
+  const int b = blockIdx.x;
+  const int job = b < g.end[0] ? 0 : (b < g.end[1] ? 1 : 2);
+  const bool waits = (c.wmask >> job) & 1;
+  if (waits && !((c.late >> job) & 1)) {
+    if (threadIdx.x == 0) {
+      const unsigned need = (unsigned)g.end[c.nsig - 1];
+      unsigned spins = 0;
+      while (chain_ld(c.w + 1) < need) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 22)) {
+          atomicOr(c.err, 1u);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (job == 0) {
+    const int r = b, xy = g.gx[0] * g.gy[0];
+    J0::run(a0, r % g.gx[0], (r % xy) / g.gx[0], r / xy, g.gx[0], lds, red4);
+  } else if (job == 1) {
+    const int r = b - g.end[0], xy = g.gx[1] * g.gy[1];
+    J1::run(a1, r % g.gx[1], (r % xy) / g.gx[1], r / xy, g.gx[1], lds, red4);
+  } else if (b < g.end[2]) {
+    const int r = b - g.end[1], xy = g.gx[2] * g.gy[2];
+    J2::run(a2, r % g.gx[2], (r % xy) / g.gx[2], r / xy, g.gx[2], lds, red4);
+  }
+  if (job < c.nsig) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(c.w + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (waits && threadIdx.x == 0) {
+    // the last waiter resets the words (every signal was counted before any waiter passed)
+    if (__hip_atomic_fetch_add(c.w + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(c.nwait - 1)) {
+      __hip_atomic_store(c.w + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c.w + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <class J0, class J1, class J2>
 struct MultiLds {
   static constexpr int BYTES = cmax(cmax(J0::LDS, J1::LDS), cmax(J2::LDS, 16));
@@ -144,6 +219,24 @@ multi_kernel_w2(const typename J0::Args a0, const typename J1::Args a1, const ty
   __shared__ uint4 lds4[MultiLds<J0, J1, J2>::BYTES / 16];
   __shared__ uint32_t red4[4];
   multi_body<J0, J1, J2>(a0, a1, a2, g, reinterpret_cast<char*>(lds4), red4);
+}
+
+template <class J0, class J1, class J2>
+__global__ void __launch_bounds__(256) multi_chain_kernel(const typename J0::Args a0, const typename J1::Args a1,
+                                                          const typename J2::Args a2, const MultiGrid g,
+                                                          const ChainArgs c) {
+  __shared__ uint4 lds4[MultiLds<J0, J1, J2>::BYTES / 16];
+  __shared__ uint32_t red4[4];
+  multi_chain_body<J0, J1, J2>(a0, a1, a2, g, c, reinterpret_cast<char*>(lds4), red4);
+}
+
+template <class J0, class J1, class J2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+multi_chain_kernel_w2(const typename J0::Args a0, const typename J1::Args a1, const typename J2::Args a2,
+                      const MultiGrid g, const ChainArgs c) {
+  __shared__ uint4 lds4[MultiLds<J0, J1, J2>::BYTES / 16];
+  __shared__ uint32_t red4[4];
+  multi_chain_body<J0, J1, J2>(a0, a1, a2, g, c, reinterpret_cast<char*>(lds4), red4);
 }
 
 }  // namespace ba3c

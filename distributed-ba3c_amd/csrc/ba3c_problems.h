@@ -48,6 +48,29 @@ __device__ __forceinline__ void relu_count_add_uniform(unsigned long long* slots
 // (atomicMax on the bits of a non-negative float orders like the float; a few tens of waves
 // per image, so the adds do not contend — one chip-wide slot measured +0.2 ms per producer).
 // Every lane of the wave must call it (wave-wide reduction).
+// Device-coherent (agent-scope: global_store / global_load sc1) accesses for data handed
+// between the jobs of one chained launch (ba3c_multi.h launch_chain): they leave / bypass the
+// XCD's non-coherent L2, so neither side needs a fence.
+__device__ __forceinline__ void st_agent_u32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent_u64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave waits until a chained launch's signal count reaches `need` (bounded: gives up with
+// bit 0 of *err set rather than hang the device).
+__device__ __forceinline__ void chain_wait_wave(const unsigned* sig, unsigned need, unsigned* err) {
+  unsigned spins = 0;
+  while (__hip_atomic_load(const_cast<unsigned*>(sig), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1u << 22)) {
+      if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);
+      break;
+    }
+  }
+}
+
 __device__ __forceinline__ void amax_publish(uint32_t* slots, int img, float m, int lane) {
   if (!slots) return;
 #pragma unroll

@@ -401,10 +401,12 @@ __global__ void __launch_bounds__(256) scalars_kernel(const float* terms, int B,
 // (s_waitcnt 0) and the workgroup barriers BEFORE thread 0 increments the counter; the last
 // workgroup reads the words only with agent-scope loads (ld_agent: global_load sc1) after its
 // barrier.  The counter itself is a device atomic.  No step relies on release/acquire ordering.
+// (bx, nblk): the workgroup's index and the grid size (a plain launch: blockIdx.x, gridDim.x;
+// a chained multi-job launch, ba3c_multi.h: the job's own)
 template <int FCH, int NZ, int AT = 0>
-__global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
+__device__ __forceinline__ void heads_body(const HeadsArgs& p, int bx, int nblk) {
   const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = bx * 4 + (threadIdx.x >> 6);
   if (n < p.B) heads_sample<FCH, NZ, AT>(p, n, lane);
   if (p.train && p.scalars) {                 // uniform over the grid
     // terms go out with st_agent and ReLU counts with device atomics; each wave waits for its
@@ -412,13 +414,18 @@ __global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
     __shared__ int last;
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(p.done, 1ull) == (unsigned long long)(gridDim.x - 1);
+    if (threadIdx.x == 0) last = atomicAdd(p.done, 1ull) == (unsigned long long)(nblk - 1);
     __syncthreads();
     if (last) {
       scalars_block(p.terms, p.B, p.beta, p.relu_count, p.scalars);
       if (threadIdx.x == 0) *p.done = 0ull;
     }
   }
+}
+
+template <int FCH, int NZ, int AT = 0>
+__global__ void __launch_bounds__(256) heads_kernel(const HeadsArgs p) {
+  heads_body<FCH, NZ, AT>(p, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -220,6 +220,14 @@ struct Conv0SArgs {
   int batch;
   const int* wexp;         // NS = 2: exponent of the weight scale
   uint32_t* amax_out;      // NS = 2: per-image max of the pooled output (may be null)
+  // chained launch (launch_prep_conv0_multi): the workgroup splits its own weight fragments
+  // from w0 (conv0/W) instead of reading wb / wexp, and waits for the zeroing workgroups'
+  // signal count (*zsig >= zneed) only before its first publication into the ReLU counters /
+  // max slots they zero
+  const float* w0;
+  const unsigned* zsig;
+  unsigned zneed;
+  unsigned* zerr;
 };
 
 // a frame byte pair -> packed 16-bit pair of the split family
@@ -322,16 +330,38 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
   if (band < nbands) load_band(band);
 
   const int li = lane & 15, lq = lane >> 4;
+  bool zdone = a.zsig == nullptr;                   // the zeroing signal seen (chained launch)
   u32x4 wf[2][2][G::KSTEPS];
-#pragma unroll
-  for (int sp = 0; sp < 2; ++sp)
+  int wx;
+  if (a.w0) {
+    // the fragments conv0s_wprep_one writes for thread lane + 64 (s + KSTEPS nt), bit for bit
+    // (LDS word 0..3 as the max reduction's scratch: the band loop's barrier precedes its use)
+    wx = amax_exp(__float_as_uint(conv0_wmax_block(a.w0, reinterpret_cast<float*>(lds))));
+    const float sc = exp2i(wx);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
-        const uint4 u = a.wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane];
-        wf[sp][nt][s] = u32x4{u.x, u.y, u.z, u.w};
+        uint32_t part[2][8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) split2(conv0_w(a.w0, s, lq, e, nt * 16 + li) * sc, part[0][e], part[1][e]);
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp)
+          wf[sp][nt][s] = u32x4{part[sp][0] | (part[sp][1] << 16), part[sp][2] | (part[sp][3] << 16),
+                                part[sp][4] | (part[sp][5] << 16), part[sp][6] | (part[sp][7] << 16)};
       }
+  } else {
+    wx = a.wexp[0];
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int s = 0; s < G::KSTEPS; ++s) {
+          const uint4 u = a.wb[((sp * 2 + nt) * G::KSTEPS + s) * 64 + lane];
+          wf[sp][nt][s] = u32x4{u.x, u.y, u.z, u.w};
+        }
+  }
   // the weights are complete before the band loop: otherwise the loop's merged wait state
   // made every band's first MFMA wait for all loads, the next band's prefetch included
 #pragma unroll
@@ -355,7 +385,7 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
 
   int pos = 0;                                      // this lane's ReLU positives (TRAIN)
   // (sum_k u8 * w 2^kw) * (2^-kw / 255): scaling by a power of two commutes with the rounding
-  const float oscale = (1.0f / 255.0f) * exp2i(-a.wexp[0]);
+  const float oscale = (1.0f / 255.0f) * exp2i(-wx);
   // Epilogue stores go through a wave-private LDS area holding one pooled row of outputs
   // (40 windows x 32 channels: 5 KB fp32 + 1.25 KB codes, contiguous in global memory too):
   // each lane writes its window / channel values there, then the wave copies the row out in
@@ -461,8 +491,13 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
       }
     }
     // max over the window maxima, then the scale: a positive scale is monotone in fp32
+    if (!zdone) {
+      chain_wait_wave(a.zsig, a.zneed, a.zerr);
+      zdone = true;
+    }
     amax_publish(a.amax_out, img, __int_as_float(bmaxi) * oscale, lane);
   }
+  if (!zdone) chain_wait_wave(a.zsig, a.zneed, a.zerr);
   if (TRAIN && a.relu_count) relu_count_add(a.relu_count, (unsigned long long)pos, lane);
 }
 

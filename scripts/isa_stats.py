@@ -22,7 +22,7 @@ def stats(text):
         if not line or line.startswith(('.', ';')) or line.endswith(':'):
             continue
         op = line.split()[0]
-        if op.startswith('v_mfma'):
+        if op.startswith(('v_mfma', 'v_smfmac')):
             c['mfma'] += 1
         elif op.startswith('v_'):
             c['valu'] += 1

@@ -10,7 +10,7 @@ import sys
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-    idx = [i for i, r in enumerate(rows) if "wprep6" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if re.search(r"wprep6|WPrep6Job", r["Kernel_Name"])]
     s, e = idx[k], idx[k + 1]
     t0 = int(rows[s]["Start_Timestamp"])
     busy = 0

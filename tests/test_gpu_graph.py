@@ -226,3 +226,58 @@ def test_one_launch_bucket_clip_matches_two_launch_clip(monkeypatch):
         del eng
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [32, 48])
+def test_chained_launches_match_separate_launches(monkeypatch, B):
+    """Chained multi-job launch (ba3c_multi.h launch_chain, default at B <= 51; BA3C_CHAIN=0:
+    two launches): the zeroing of the ReLU counters / max slots signals inside the launch, and
+    conv0's forward splits its own weight fragments and waits for it only before publishing.
+    Outputs must be bit-identical: training gradients and scalars over repeated steps (the
+    counter words reset at every launch's end), the predictor's probabilities and values, graph
+    replays at B=32; no wait gave up."""
+    from ba3c_amd.engine import Ba3cEngine
+    rs = np.random.RandomState(B)
+    batches = []
+    for _ in range(3):
+        batches.append((torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda(),
+                        torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda(),
+                        torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()))
+    params = O.init_params(128, 4, 4, seed=9, dtype=np.float32)
+    out = []
+    for env in ("0", None):
+        if env is None:
+            monkeypatch.delenv("BA3C_CHAIN", raising=False)
+        else:
+            monkeypatch.setenv("BA3C_CHAIN", env)
+        eng = Ba3cEngine(num_actions=4, fc_neurons=128, fc_splits=4, max_batch=B)
+        eng.load_params(params)
+        got = []
+        for state, action, R in batches:
+            sc = eng.train_grads(state, action, R)
+            got += [eng.grads.clone(), sc.clone()]
+            probs, probsT, value = eng.forward(state)
+            got += [probs.clone(), probsT.clone(), value.clone()]
+        torch.cuda.synchronize()
+        assert eng.device_errors() == 0
+        out.append(got)
+        del eng
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+    if B == 32:
+        monkeypatch.setenv("BA3C_CHAIN", "0")
+        plain = _trainer(B)
+        monkeypatch.delenv("BA3C_CHAIN")
+        cap = _trainer(B)
+        bs = _batches(B, 4)
+        for b in bs[1:]:
+            plain.train_step(*b)
+        static = tuple(t.clone() for t in bs[0])
+        replay = cap.capture_step(*static, warmup=2)
+        for b in bs[1:]:
+            for dst, src in zip(static, b):
+                dst.copy_(src)
+            replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(cap.engine.params.cpu().numpy(), plain.engine.params.cpu().numpy())
+        assert cap.engine.device_errors() == 0
