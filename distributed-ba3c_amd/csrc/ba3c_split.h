@@ -230,6 +230,17 @@ struct Conv0SArgs {
   unsigned* zerr;
 };
 
+// 1 if the fp32 bits x are a positive value (x > 0 as a signed integer), else 0: one
+// v_med3_i32 (x, 0, 1); in C the clamp is turned back into a compare + select through VCC.
+// x is an MFMA result: inline asm is not seen by the MFMA -> VALU read hazard check, so the
+// asm also takes `after`, a compiler-visible VALU result of the same accumulator (the window
+// max), which orders it behind the wait states the compiler inserted for that read.
+__device__ __forceinline__ int c0w_pos1(int x, int after) {
+  int r;
+  asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(x), "v"(after));
+  return r;
+}
+
 // a frame byte pair -> packed 16-bit pair of the split family
 template <int NS>
 __device__ __forceinline__ uint32_t u8pair(uint32_t a, uint32_t b) {
@@ -459,7 +470,9 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
             // ReLU positives: the bits compare as signed integers (x > 0 exactly for x > 0).
             // Per-lane compare + add; a v_cmp -> SGPR ballot + s_bcnt1 form has fewer VALU
             // instructions but measured slower (0.189 -> 0.209 ms, VALU-to-SALU dependencies)
-            pos += (b0 > 0) + (b1 > 0) + (b2 > 0) + (b3 > 0);
+            // (x > 0) as med3(x, 0, 1) on the bits (v_med3_i32) and three-input adds: no VCC
+            // round trips (a compare + add-with-carry per value chained the four through VCC)
+            pos += (c0w_pos1(b0, m) + c0w_pos1(b1, m)) + (c0w_pos1(b2, m) + c0w_pos1(b3, m));
             // materialise the count here: otherwise it is sunk to its only use after the band
             // loop, keeping every accumulator of the chunk live (r03g: > 256 registers)
             asm volatile("" : "+v"(pos));
