@@ -200,9 +200,10 @@ int ba3c_greedy(void* stream, const float* probs, const double* u, const int64_t
  * recorded events and returns the summed milliseconds and launch count since enabling. */
 int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
 /* Device-side error flags of the handle's in-launch waits (bit 0: a fused clip+optimizer launch,
- * bit 1: a one-launch ba3c_clip_grads_range, stopped waiting for another workgroup's partial —
- * its results are invalid).  0 in normal operation.  Synchronises the device (diagnostics /
- * tests only). */
+ * bit 1: a one-launch ba3c_clip_grads_range, stopped waiting for another workgroup's partial;
+ * bit 2: a chained launch's conv0 workgroups stopped waiting for the zeroing of the ReLU
+ * counters / max slots — the results are invalid).  0 in normal operation.  Synchronises the
+ * device (diagnostics / tests only). */
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags);
 
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
