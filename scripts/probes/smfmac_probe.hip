@@ -65,6 +65,25 @@ __global__ void rate(const f16x8* a, const f16x16* b, const int* idx, f32x4* c, 
   c[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// dependent chains: NACC accumulators round-robin (NACC = 1: every smfmac waits for the
+// previous one's result)
+template <int NACC>
+__global__ void chain(const f16x8* a, const f16x16* b, const int* idx, f32x4* c, int iters) {
+  const int l = threadIdx.x & 63;
+  f16x8 av = a[l];
+  f16x16 bv = b[l];
+  const int ix = idx[l];
+  f32x4 acc[NACC];
+  for (int j = 0; j < NACC; ++j) acc[j] = f32x4{0, 0, 0, 0};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k % NACC] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av, bv, acc[k % NACC], ix, 0, 0);
+  }
+  f32x4 s = acc[0];
+  for (int j = 1; j < NACC; ++j) s += acc[j];
+  c[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 static int kA(int hyp, int lane, int e) {  // logical K of lane's logical A element e (0..15)
   const int g = lane >> 4;
   return hyp == 0 ? 16 * g + e : (e < 8 ? 8 * g + e : 32 + 8 * g + (e - 8));
@@ -200,5 +219,23 @@ int main() {
     printf("smfmac_16x16x32_f16: %.3f ms, %.1f logical TFLOP/s, %.2f ns per wave-instruction per SIMD\n", ms,
            n * 16.0 * 16 * 32 * 2 / ms / 1e9, ms * 1e6 / (n / 1024.0));
   }
+  // dependent-chain rate: one wave per SIMD (256 workgroups x 256 threads) and 2 per SIMD
+  for (int wps = 1; wps <= 2; ++wps)
+    for (int nacc : {1, 2, 3, 4, 8}) {
+      hipEventRecord(e0);
+      const int nb = 256 * wps;
+      switch (nacc) {
+        case 1: chain<1><<<nb, 256>>>(da, db, di, dc, iters); break;
+        case 2: chain<2><<<nb, 256>>>(da, db, di, dc, iters); break;
+        case 3: chain<3><<<nb, 256>>>(da, db, di, dc, iters); break;
+        case 4: chain<4><<<nb, 256>>>(da, db, di, dc, iters); break;
+        default: chain<8><<<nb, 256>>>(da, db, di, dc, iters); break;
+      }
+      hipEventRecord(e1); hipEventSynchronize(e1);
+      float ms; hipEventElapsedTime(&ms, e0, e1);
+      const double n = (double)nb * 4 * iters * 8;   // wave-instructions
+      printf("smfmac_16x16x64 chain: %d waves/SIMD, %d accumulators: %.2f ns per wave-instruction per SIMD\n",
+             wps, nacc, ms * 1e6 / (n / 1024.0));
+    }
   return 0;
 }
