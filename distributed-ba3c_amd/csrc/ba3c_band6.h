@@ -703,6 +703,54 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
     band6r_body<L, PRE_>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
 }
 
+// conv1's 2:4-sparse input gradient (ba3c_dgrad1s.h): geometry and the B operand of its
+// sparse logical K order, prepared by wprep job WJ_C1S
+struct D1S {
+  static constexpr int HO = 40, WO = 40, C = 32, O = 32, UP = 18;  // dX map / channels; pooled dY
+  static constexpr int RB = 4, NBANDS = HO / RB;                     // output rows per band
+  static constexpr int SR = RB + 4;                                  // staged dY rows
+  static constexpr int NW = 22;                                      // windows (w' = w + 2)
+  // PV: dword (window w', window w' + 1) per staged row, w' 0..20, channel; MV: the masked value
+  // of window w', w' 0..21, channel (single taps); the quad indices per POOLED row.  Pitches from
+  // a bank search over the A-read lane maps (conflict-free ds_read_b128)
+  static constexpr int PV_WS = 40, PV_RS = 864;
+  static constexpr int MV_WS = 16, MV_RS = 360;
+  static constexpr int PV_PLANE = SR * PV_RS, MV_PLANE = SR * MV_RS;  // dwords
+  static constexpr int IXF_RS = 21 * 8, IXS_RS = NW * 4;             // u16 per pooled row
+  static constexpr int MV_OFF = 2 * PV_PLANE * 4;                    // bytes
+  static constexpr int IXF_OFF = MV_OFF + 2 * MV_PLANE * 4;
+  static constexpr int IXS_OFF = IXF_OFF + (SR / 2) * IXF_RS * 2;
+  static constexpr int LDS_BYTES = IXS_OFF + (SR / 2) * IXS_RS * 2;
+  static constexpr int KSTEPS = 15;                                  // 5 tap rows x 3
+  static constexpr int WFRAG = 16;                                   // halves per lane and plane
+  static constexpr int WPLANE = 2 * KSTEPS * 2 * 64 * WFRAG;         // halves per plane (2 parities)
+  static constexpr int NITEM = (SR / 2) * NW * (O / 4);              // (pooled row, window, 4 ch)
+  static constexpr int IPT = (NITEM + 255) / 256;
+  static_assert(2 * LDS_BYTES <= 160 * 1024 && 21 * PV_WS <= PV_RS && NW * MV_WS <= MV_RS,
+                "d1s layout: two workgroups per CU");
+};
+
+// The weight of B element (parity eps, k-step s, column c, logical K) — the wprep job's value
+// (scripts/probes/sparse_dgrad_model.py bweight): W is conv1/W [5][5][C][O] (HWIO).
+__device__ __forceinline__ float d1s_weight(const float* __restrict__ w, int eps, int s, int c, int K) {
+  const int kh = s / 3, t = s - 3 * kh, q = K >> 2, p = K & 3;
+  if (t < 2) {                                     // aligned quad: channel 16 t + q, tap kw = p + eps
+    const int o = 16 * t + q, kw = p + eps;
+    return w[((size_t)((4 - kh) * 5 + (4 - kw)) * D1S::C + c) * D1S::O + o];
+  }
+  const int o = 2 * q + (p >> 1), cl = p & 1;      // single taps: channel pair, pixel column cl
+  if (eps == 0) return cl == 0 ? w[((size_t)((4 - kh) * 5 + 0) * D1S::C + c) * D1S::O + o] : 0.f;
+  return cl == 1 ? w[((size_t)((4 - kh) * 5 + 4) * D1S::C + c) * D1S::O + o] : 0.f;
+}
+// fragment element d of one plane: [eps][s][n-tile][lane][16]; B lane layout of the 16x16x64
+// sparse MFMA: column lane & 15, logical K 8 g + e (e < 8) / 32 + 8 g + e - 8 (g = lane >> 4)
+__device__ __forceinline__ float d1s_wprep_value(const float* __restrict__ w, int d) {
+  const int e = d & 15, lane = (d >> 4) & 63, nt = (d >> 10) & 1, rest = d >> 11;
+  const int s = rest % D1S::KSTEPS, eps = rest / D1S::KSTEPS, g = lane >> 4;
+  const int K = e < 8 ? 8 * g + e : 32 + 8 * g + (e - 8);
+  return d1s_weight(w, eps, s, 16 * nt + (lane & 15), K);
+}
+
 // One launch per step for all weight preparation on the split path: job y < njobs writes the
 // NS split planes of band-conv copy y straight from the parameters (no fp32 [N][K] copy and no
 // second pass), job y == njobs (when w0 is set) prepares conv0's MFMA B fragments.  With the
@@ -712,7 +760,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
 struct WPrep6Args {
   WPrepArgs jobs;
   uint16_t* wt6;
-  int off[6];              // fp32 offset of job i; its splits start at NS * off[i]
+  int off[7];              // fp32 offset of job i; its splits start at NS * off[i]
   const float* w0;         // conv0/W (null: no conv0 job)
   uint4* wb0;
   unsigned long long* relu;  // training: ReLU-count slots zeroed here (no separate memset)
@@ -753,7 +801,7 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
     auto amax4 = [](float m, const float4& v) {
       return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
     };
-    const int n4 = j.n / 4;
+    const int n4 = (j.dgrad == 2 ? j.KH * j.KW * j.CI * j.CO : j.n) / 4;   // the source tensor
     float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
     int i = threadIdx.x;
     for (; i + 768 < n4; i += 1024) {
@@ -774,6 +822,15 @@ __device__ __forceinline__ void wprep6_body(const WPrep6Args& a, int bx, int by,
     sc = exp2i(k);
   }
   uint16_t* dst = a.wt6 + 2 * (size_t)a.off[y];
+  if (j.dgrad == 2) {                  // conv1's sparse input-gradient fragments (ba3c_dgrad1s.h)
+    for (int d = bx * 256 + threadIdx.x; d < j.n; d += gx * 256) {
+      uint32_t hi, lo;
+      split2(d1s_wprep_value(j.w, d) * sc, hi, lo);
+      dst[d] = (uint16_t)hi;
+      dst[j.n + d] = (uint16_t)lo;
+    }
+    return;
+  }
   // destination d in the band kernels' MFMA B-fragment order [K / 32][N / 16][lane][8]: lane
   // (lq, li) holds column n = 16 nb + li, K = 32 k32 + 8 lq .. + 7 (Band6Ops::compute)
   const int K = j.KH * j.KW * (j.dgrad ? j.CO : j.CI);

@@ -19,6 +19,7 @@
 #include "ba3c_band6.h"
 #include "ba3c_conv.h"
 #include "ba3c_conv3.h"
+#include "ba3c_dgrad1s.h"
 #include "ba3c_gemm6.h"
 #include "ba3c_launch.h"
 #include "ba3c_multi.h"
@@ -143,6 +144,12 @@ struct ba3c_handle {
   // unchained launches).  BA3C_CHAIN=0: unchained.
   bool chain_on = true;
   unsigned* chain = nullptr;
+  // conv1's input gradient on 2:4-sparse MFMA (ba3c_dgrad1s.h) at the ring-walk batches
+  // (B >= 2 x CUs) with BA3C_C1D_SPARSE=1; default 0, the dense ring walk: the sparse kernel
+  // issues 40 % fewer matrix instructions but measured 0.40 against 0.33 ms (r05x-y: its L2
+  // weight-fragment stream and its staging, which two workgroups per CU do not hide, cost
+  // 0.07 and 0.13 ms)
+  bool c1s = false;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -228,7 +235,7 @@ inline int conv3_wgrad_p(int B, int cus) { return std::min(B, std::min(C3W_P, cu
 constexpr int WG_P0S = 512;   // conv0s_wgrad_kernel: 52 KB LDS, two workgroups per CU
 constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C3F = WT_C2F + 800 * 64,
               WT_C1D = WT_C3F + 576 * 64, WT_C2D = WT_C1D + 800 * 32, WT_C3D = WT_C2D + 1600 * 32,
-              WT_C0F = WT_C3D + 576 * 64,
+              WT_C1S = WT_C3D + 576 * 64, WT_C0F = WT_C1S + D1S::WPLANE,
               WT_C0S = WT_C0F + 32 * Conv0Geom::KDIM,            // uint4 [Conv0S::WB_U4]
               WT_TOTAL = WT_C0S + 4 * Conv0S::WB_U4;
 
@@ -249,7 +256,8 @@ struct Workspace {
 enum { AM_P0 = 0, AM_P1 = 1, AM_DP0 = 2, AM_DP1 = 3, AM_DP2 = 4, AM_P2 = 5, AM_DY3 = 6, AMAX_N = 7 };
 // weight-preparation jobs (forward copies first: inference prepares only those) and the
 // index of each one's scale exponent in Workspace::wexp
-enum { WJ_C1F = 0, WJ_C2F = 1, WJ_C3F = 2, WJ_C1D = 3, WJ_C2D = 4, WJ_C3D = 5, WJ_N = 6, WJ_FWD = 3, WX_CONV0 = 7 };
+enum { WJ_C1F = 0, WJ_C2F = 1, WJ_C3F = 2, WJ_C1D = 3, WJ_C2D = 4, WJ_C3D = 5, WJ_C1S = 6, WJ_N = 7, WJ_FWD = 3,
+       WX_CONV0 = 7 };
 
 struct WgradPlan {
   int M, N, K, S, kchunk, mt, nt;
@@ -559,7 +567,10 @@ int reduce_wgrad6(ba3c_handle* h, hipStream_t s, const Wg6Args& a, int P, float*
 
 // Split-path weight preparation arguments (wprep6_kernel): every job, the conv0 fragments and
 // the zeroing of the ReLU counters / max slots.
-WPrep6Args wprep6_args(ba3c_handle* h, const float* prm, const Workspace& w, bool train) {
+// conv1's sparse input gradient at this batch (the ring-walk batches)
+bool use_c1s(const ba3c_handle* h, int B) { return h->c1s && h->band && h->ring && B >= 2 * h->cus; }
+
+WPrep6Args wprep6_args(ba3c_handle* h, const float* prm, const Workspace& w, bool train, bool c1s = false) {
   const float* W1 = prm + h->tensors[h->idx_conv[1]].offset;
   const float* W2 = prm + h->tensors[h->idx_conv[2]].offset;
   const float* W3 = prm + h->tensors[h->idx_conv[3]].offset;
@@ -571,9 +582,10 @@ WPrep6Args wprep6_args(ba3c_handle* h, const float* prm, const Workspace& w, boo
   a.job[WJ_C1D] = WPrepJob{W1, w.wt + WT_C1D, 5, 5, 32, 32, 1, 800 * 32};
   a.job[WJ_C2D] = WPrepJob{W2, w.wt + WT_C2D, 5, 5, 32, 64, 1, 1600 * 32};
   a.job[WJ_C3D] = WPrepJob{W3, w.wt + WT_C3D, 3, 3, 64, 64, 1, 576 * 64};
-  a.njobs = train ? WJ_N : WJ_FWD;
+  a.job[WJ_C1S] = WPrepJob{W1, w.wt + WT_C1S, 5, 5, 32, 32, 2, D1S::WPLANE};
+  a.njobs = train ? (c1s ? WJ_N : WJ_C1S) : WJ_FWD;
   pa.wt6 = w.wt6;
-  const int offs[WJ_N] = {WT_C1F, WT_C2F, WT_C3F, WT_C1D, WT_C2D, WT_C3D};
+  const int offs[WJ_N] = {WT_C1F, WT_C2F, WT_C3F, WT_C1D, WT_C2D, WT_C3D, WT_C1S};
   for (int j = 0; j < WJ_N; ++j) pa.off[j] = offs[j];
   pa.w0 = prm + h->tensors[h->idx_conv[0]].offset;
   pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
@@ -625,8 +637,8 @@ int launch_prep_conv0_multi(ba3c_handle* h, hipStream_t s, const float* prm, con
 
 // split planes of the band-conv weights for this step (forward; + rotated dgrad in training)
 // and, for C == 4, conv0's MFMA B fragments: one launch
-int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, bool train) {
-  WPrep6Args pa = wprep6_args(h, prm, w, train);
+int launch_wprep(ba3c_handle* h, hipStream_t s, const float* prm, const Workspace& w, bool train, int B) {
+  WPrep6Args pa = wprep6_args(h, prm, w, train, use_c1s(h, B));
   const bool c0s = h->cfg.channels == 4;
   if (!c0s) pa.w0 = nullptr;
   hipLaunchKernelGGL(wprep6_kernel, dim3(64, pa.jobs.njobs + (c0s ? 1 : 0)), dim3(256), 0, s, pa);
@@ -691,7 +703,7 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
     if (mj) {
       CHECK(launch_prep_conv0_multi(h, s, prm, state, B, w, train));
     } else {
-      CHECK(launch_wprep(h, s, prm, w, train));
+      CHECK(launch_wprep(h, s, prm, w, train, B));
       if constexpr (CH == 4) {
         CHECK(launch_conv0_band(h, s, BandArgs{reinterpret_cast<const float*>(state), nullptr, nullptr, w.p0, c0,
                                                rc, B}, w));
@@ -1040,6 +1052,15 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     }
     if (paired) {
       // both gradients ran in the multi-job launch above
+    } else if (use_c1s(h, B)) {
+      // 2:4-sparse MFMA (ba3c_dgrad1s.h): two workgroups per CU, persistent over bands
+      const Band6Args b = band6_args<typename LY::C1D>(h, BandArgs{w.dp1, w.c1, nullptr, w.dp0, nullptr, nullptr, B},
+                                                       w, WT_C1S, SplitIO{AM_DP1, WJ_C1S, AM_DP0});
+      {
+        ProbeScope ps(h, s, BA3C_K_CONV1_DGRAD);
+        hipLaunchKernelGGL(dgrad1s_kernel, dim3(2 * h->cus), dim3(256), 0, s, b);
+      }
+      HIP_TRY(hipGetLastError());
     } else if (h->band) {
       const BandArgs ba{w.dp1, w.c1, nullptr, w.dp0, nullptr, nullptr, B};
       CHECK(launch_band6<typename LY::C1D>(h, s, BA3C_K_CONV1_DGRAD, ba, w, WT_C1D, SplitIO{AM_DP1, WJ_C1D, AM_DP0},
@@ -1190,10 +1211,11 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   };
   static const Switch kSwitches[] = {{"BA3C_GENERIC", 0, 1},  {"BA3C_C1PAIR", 0, 2},   {"BA3C_SCALARS_RIDE", 0, 1},
                                      {"BA3C_OVERLAP", 0, 2},  {"BA3C_MULTI", 0, 1},    {"BA3C_MULTI_BIG", 0, 3},
-                                     {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}, {"BA3C_CHAIN", 0, 1}};
-  constexpr int NSW = 9;
+                                     {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}, {"BA3C_CHAIN", 0, 1},
+                                     {"BA3C_C1D_SPARSE", 0, 1}};
+  constexpr int NSW = 10;
   int sw[NSW];
-  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1};
+  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1, 0};
   for (int i = 0; i < NSW; ++i) {
     sw[i] = defaults[i];
     const char* e = getenv(kSwitches[i].name);
@@ -1214,6 +1236,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   h->fused_update = sw[6] != 0;
   h->ring = sw[7] != 0;
   h->chain_on = sw[8] != 0;
+  h->c1s = sw[9] != 0;
   h->g6 = h->band;
   {
     int dev = 0, n = 0;

@@ -71,10 +71,10 @@ struct Conv0Geom {
 struct WPrepJob {
   const float* w;
   float* wt;
-  int KH, KW, CI, CO, dgrad, n;   // n = total elements
+  int KH, KW, CI, CO, dgrad, n;   // n = total elements; dgrad 2: conv1's sparse input gradient
 };
 struct WPrepArgs {
-  WPrepJob job[6];
+  WPrepJob job[7];
   int njobs;
 };
 

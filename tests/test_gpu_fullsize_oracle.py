@@ -37,9 +37,11 @@ def _case(frames):
     return params, state, action, R
 
 
-@pytest.mark.parametrize("frames", ["random", "atari"])
-def test_bench_workload_every_gradient_matches_fp64(frames):
+@pytest.mark.parametrize("frames,sparse", [("random", "0"), ("atari", "0"), ("random", "1")])
+def test_bench_workload_every_gradient_matches_fp64(monkeypatch, frames, sparse):
+    """sparse = 1: conv1's input gradient on 2:4-sparse MFMA (BA3C_C1D_SPARSE=1, ba3c_dgrad1s.h)."""
     from ba3c_amd.engine import Ba3cEngine
+    monkeypatch.setenv("BA3C_C1D_SPARSE", sparse)
     params, state, action, R = _case(frames)
     eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=B)
     eng.load_params(params)
@@ -66,8 +68,8 @@ def test_bench_workload_every_gradient_matches_fp64(frames):
 
     ref, out = loss_and_grads_forced(params, state, action, R, CFG, forced, chunk=256)
     errs = {k: rel(got[k], ref[k]) for k in ref}
-    print("per-tensor rel err vs fp64 (%s frames): %s" % (
-        frames, ", ".join("%s %.2e" % kv for kv in sorted(errs.items()))))
+    print("per-tensor rel err vs fp64 (%s frames, sparse conv1 dgrad %s): %s" % (
+        frames, sparse, ", ".join("%s %.2e" % kv for kv in sorted(errs.items()))))
     bad = {k: e for k, e in errs.items() if e >= GRAD_TOL}
     assert not bad, bad
     assert np.all(got["conv0/W"][:, :, 4:, :] == 0)

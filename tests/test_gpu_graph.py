@@ -131,8 +131,10 @@ def test_large_batch_fc1_multi_job_matches_separate_launches(monkeypatch):
 def test_ring_walk_band_kernels_match_one_band_kernels(monkeypatch):
     """From B = 2 x CUs up, conv1's forward and input gradient run as ring-walk persistent
     kernels (whole images per workgroup, halo rows carried in LDS) instead of one band per
-    workgroup (BA3C_RING=0): activations, dp0, gradients and scalars bit for bit equal."""
+    workgroup (BA3C_RING=0): activations, dp0, gradients and scalars bit for bit equal (conv1's
+    input gradient dense on both sides: BA3C_C1D_SPARSE=0)."""
     from ba3c_amd.engine import Ba3cEngine
+    monkeypatch.setenv("BA3C_C1D_SPARSE", "0")
     B = 2 * torch.cuda.get_device_properties(0).multi_processor_count
     rs = np.random.RandomState(78)
     state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
@@ -155,6 +157,57 @@ def test_ring_walk_band_kernels_match_one_band_kernels(monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
     for n in out[0][2]:
         assert torch.equal(out[0][2][n], out[1][2][n]), n
+
+
+@pytest.mark.parametrize("frames", ["random", "atari"])
+def test_sparse_conv1_input_gradient_matches_dense(monkeypatch, frames):
+    """conv1's input gradient on 2:4-sparse MFMA (ba3c_dgrad1s.h, BA3C_C1D_SPARSE=1, used from
+    B = 2 x CUs; off by default: slower) against the dense ring walk (BA3C_C1D_SPARSE=0, the
+    default) on the same inputs: the same products minus
+    exact zeros, summed in another order — dP0 within 4e-6 of the dense one (normwise, per
+    image; both are fp32-class, ~1e-6 apart), conv0/W's gradient (the only tensor dP0 feeds) within 1e-5, every other gradient,
+    the scalars, p1 and the codes bit for bit."""
+    from atari_frames import atari_frames
+    from ba3c_amd.engine import Ba3cEngine
+    B = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    rs = np.random.RandomState(81)
+    if frames == "random":
+        state = rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)
+        params = O.init_params(512, 1, 4, seed=8, dtype=np.float32)
+    else:
+        state = atari_frames(B, 81)
+        params = {k: (v * np.float32(2.0)).astype(np.float32)
+                  for k, v in O.init_params(512, 1, 4, seed=8, dtype=np.float32).items()}
+    state = torch.from_numpy(state).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("BA3C_C1D_SPARSE", env)
+        eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=B)
+        eng.load_params(params)
+        sc = eng.train_grads(state, action, R)
+        ws = {n: eng.workspace_tensor(n, B).clone() for n in ("p1", "c1", "dp0")}
+        g = {k: v.copy() for k, v in eng.state_dict(eng.grads).items()}
+        torch.cuda.synchronize()
+        out.append((g, sc.clone(), ws))
+        assert eng.device_errors() == 0
+        del eng
+    (gd, sd, wd), (gs, ss, wsp) = out
+    assert torch.equal(sd, ss)
+    assert torch.equal(wd["p1"], wsp["p1"]) and torch.equal(wd["c1"], wsp["c1"])
+    d = wd["dp0"].double().reshape(B, -1).cpu().numpy()
+    e = wsp["dp0"].double().reshape(B, -1).cpu().numpy()
+    err = np.abs(e - d).max(axis=1) / np.maximum(np.abs(d).max(axis=1), 1e-30)
+    print("dp0 per-image rel err: max %.2e" % err.max())
+    assert err.max() < 4e-6, err.max()
+    for k in gd:
+        if k == "conv0/W":
+            r = np.abs(gs[k] - gd[k]).max() / np.abs(gd[k]).max()
+            print("conv0/W rel err %.2e" % r)
+            assert r < 1e-5, r
+        else:
+            assert np.array_equal(gs[k], gd[k]), k
 
 
 @pytest.mark.parametrize("B", [32, 160])
