@@ -148,7 +148,8 @@ class Ba3cEngine(object):
     def train_grads(self, state, action, futurereward, entropy_beta=0.01, grads=None, phase=0):
         """Forward + loss + backward; raw gradients into `grads` (default self.grads).
         Returns the device float64 scalars tensor (order: _lib.SCALAR_NAMES).  phase 1 / 2
-        split the pass at the fc1 + heads bucket (ba3c_train_grads_phase)."""
+        split the pass at the fc1 + heads bucket (ba3c_train_grads_phase); phase 3 leaves the
+        final gradient reduction to the next fused-clip apply_update (one launch fewer)."""
         B = self._check_state(state)
         assert action.dtype == torch.int64 and action.shape == (B,) and action.is_cuda
         assert futurereward.dtype == torch.float32 and futurereward.shape == (B,)

@@ -6,6 +6,7 @@ gradient processors (fused clip), the synchronous RCCL gradient mean when
 SyncReplicasOptimizer is used, and one fused optimizer apply; it returns the TfDictOp
 dictionary of the reference (multigpu.py:193-205).
 """
+import os
 import time
 
 import numpy as np
@@ -78,6 +79,11 @@ class Ba3cTrainer(object):
                             and isinstance(procs[0].func, ClipByAverageNorm)
                             and procs[0].regex == ".*$")
         self._procs = procs
+        # BA3C_DEFER_REDUCE=1 (single replica): the pass's weight-gradient reduction rides on the
+        # fused apply's launch (ba3c_train_grads_phase phase 3: one launch fewer).  Default off:
+        # same-box r05ab, B=32 step 0.1607 -> 0.1646 ms, B=2048 1.743 -> 1.752 ms (the hand-off's
+        # agent-scope stores / loads and signal counters cost more than the launch boundary)
+        self._defer_reduce = os.environ.get("BA3C_DEFER_REDUCE", "0") == "1"
         if isinstance(self.optimizer, SyncReplicasOptimizer):
             self.optimizer.broadcast_variables(self.engine)
 
@@ -124,7 +130,12 @@ class Ba3cTrainer(object):
             self._bucketed_sync_step(state, action, futurereward)
             self.global_step += 1
             return
-        self.model.build_graph([state, action, futurereward])
+        if self._defer_reduce and self._fused_clip and not isinstance(opt, SyncReplicasOptimizer):
+            self.model.train_phase = 3
+        try:
+            self.model.build_graph([state, action, futurereward])
+        finally:
+            self.model.train_phase = 0
         if isinstance(opt, SyncReplicasOptimizer):
             if self._fused_clip:
                 opt.aggregate(self.engine)

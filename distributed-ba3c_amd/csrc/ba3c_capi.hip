@@ -80,7 +80,8 @@ struct TensorDesc {
   int32_t ndim;
 };
 
-constexpr int CHAIN_SITES = 1;   // chained launch sites (launch_chain)
+constexpr int CHAIN_SITES = 2;   // chained launch sites (launch_chain)
+constexpr int CHAIN_SPREAD = 32; // spread signal counters of a site with many signalling workgroups
 
 struct ba3c_handle {
   ba3c_config cfg;
@@ -144,12 +145,20 @@ struct ba3c_handle {
   // unchained launches).  BA3C_CHAIN=0: unchained.
   bool chain_on = true;
   unsigned* chain = nullptr;
+  unsigned* spread = nullptr;   // CHAIN_SPREAD counters, CHAIN_STRIDE words apart (64-byte aligned)
   // conv1's input gradient on 2:4-sparse MFMA (ba3c_dgrad1s.h) at the ring-walk batches
   // (B >= 2 x CUs) with BA3C_C1D_SPARSE=1; default 0, the dense ring walk: the sparse kernel
   // issues 40 % fewer matrix instructions but measured 0.40 against 0.33 ms (r05x-y: its L2
   // weight-fragment stream and its staging, which two workgroups per CU do not hide, cost
   // 0.07 and 0.13 ms)
   bool c1s = false;
+  // ba3c_train_grads_phase(phase 3): the pass's weight-gradient reduction is left pending and
+  // the next fused-clip apply on the handle runs it as the signalling job of a chained launch
+  // (reduce -> clip + update, one launch fewer); any other entry point launches it first
+  bool pend_reduce = false;
+  hipStream_t pend_stream = nullptr;
+  const float* pend_grads = nullptr;
+  bool defer_final = false;   // set by train_grads_impl for phase 3
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -479,13 +488,13 @@ int launch_multi(hipStream_t s, const typename J0::Args& a0, dim3 g0, const type
 // A chained multi-job launch (ba3c_multi.h): jobs [0, nsig) signal, the jobs in `wmask` wait
 // for them (those in `late` inside their body); `site` picks the launch site's counter words.
 // Callers check chain_ok() first.
-constexpr int CHAIN_PREP_CONV0 = 0;
+constexpr int CHAIN_PREP_CONV0 = 0, CHAIN_REDUCE_UPDATE = 1;
 bool chain_ok(const ba3c_handle* h) { return h->chain_on && h->chain != nullptr; }
 
 template <bool W2, class J0, class J1, class J2 = NoJob>
 int launch_chain(hipStream_t s, int site, int nsig, int wmask, int late, const typename J0::Args& a0, dim3 g0,
                  const typename J1::Args& a1, dim3 g1, const typename J2::Args& a2 = typename J2::Args{},
-                 dim3 g2 = dim3(0, 1, 1), ba3c_handle* h = nullptr, int kid = -1) {
+                 dim3 g2 = dim3(0, 1, 1), ba3c_handle* h = nullptr, int kid = -1, bool spread = false) {
   MultiGrid g;
   const dim3 gs[3] = {g0, g1, g2};
   int end = 0;
@@ -499,7 +508,8 @@ int launch_chain(hipStream_t s, int site, int nsig, int wmask, int late, const t
   int nwait = 0;
   for (int j = 0; j < 3; ++j)
     if ((wmask >> j) & 1) nwait += g.end[j] - (j ? g.end[j - 1] : 0);
-  const ChainArgs c{h->chain + 4 * site, h->chain + 4 * CHAIN_SITES, nsig, wmask, nwait, late};
+  const ChainArgs c{h->chain + 4 * site, h->chain + 4 * CHAIN_SITES, nsig, wmask, nwait, late,
+                    h->spread, spread ? CHAIN_SPREAD : 0};
   std::optional<ProbeScope> probe;
   if (kid >= 0) probe.emplace(h, s, kid);
   if constexpr (W2)
@@ -830,7 +840,11 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
     }
     const ReduceJobs& jb = h->rjobs;
-    if (jb.n > 0) {
+    if (jb.n > 0 && h->defer_final && phase == 0) {
+      h->pend_reduce = true;   // the next fused apply runs it (flush_reduce otherwise)
+      h->pend_stream = s;
+      h->pend_grads = grads;
+    } else if (jb.n > 0) {
       ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
       hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(256), 0, s, jb);
     }
@@ -1305,7 +1319,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   // clip_update_kernel's and clip_range_kernel's tagged partials + error words (no device:
   // stay null, two-launch paths)
   const size_t ubytes = ((size_t)tt.nchunks + 1) * sizeof(unsigned long long);
-  const size_t cbytes = (4 * CHAIN_SITES + 4) * sizeof(unsigned);
+  const size_t cbytes = (4 * CHAIN_SITES + 4 + CHAIN_SPREAD * CHAIN_STRIDE + 16) * sizeof(unsigned);
   if (hipMalloc(reinterpret_cast<void**>(&h->utag), 2 * ubytes + cbytes) != hipSuccess) {
     h->utag = nullptr;
     (void)hipGetLastError();
@@ -1316,6 +1330,8 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   } else {
     h->ctag = h->utag + tt.nchunks + 1;
     h->chain = reinterpret_cast<unsigned*>(h->ctag + tt.nchunks + 1);
+    const uintptr_t sp = reinterpret_cast<uintptr_t>(h->chain + 4 * CHAIN_SITES + 4);
+    h->spread = reinterpret_cast<unsigned*>((sp + 63) & ~uintptr_t(63));
   }
   *out = h;
   return BA3C_OK;
@@ -1381,6 +1397,8 @@ size_t ba3c_workspace_size(const ba3c_handle* h, int32_t batch, int32_t train) {
   return carve(h, nullptr, batch, train != 0).bytes;
 }
 
+static int flush_reduce(ba3c_handle* h);
+
 int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                  int32_t batch, float explore_factor, void* workspace, float* probs,
                  float* probsT, float* value) {
@@ -1388,6 +1406,7 @@ int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_
     return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  CHECK(flush_reduce(h));
   Workspace w = carve(h, workspace, batch, false);
   std::memset(h->merged, 0, sizeof(h->merged));
   int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, false)
@@ -1402,6 +1421,18 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
                             float entropy_beta, void* workspace, float* grads, double* scalars,
                             int32_t phase);
 
+// launch a reduction a phase-3 pass left pending (on its own stream: stream order keeps it
+// ahead of whatever the caller issues after the pass on that stream)
+static int flush_reduce(ba3c_handle* h) {
+  if (!h || !h->pend_reduce) return BA3C_OK;
+  h->pend_reduce = false;
+  const ReduceJobs& jb = h->rjobs;
+  ProbeScope ps(h, h->pend_stream, BA3C_K_WGRAD_REDUCE);
+  hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(256), 0, h->pend_stream, jb);
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
 int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                      const int64_t* action, const float* futurereward, int32_t batch,
                      float entropy_beta, void* workspace, float* grads, double* scalars) {
@@ -1413,9 +1444,15 @@ int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, co
                            const int64_t* action, const float* futurereward, int32_t batch,
                            float entropy_beta, void* workspace, float* grads, double* scalars,
                            int32_t phase) {
-  if (phase < 0 || phase > 2) return fail(BA3C_ERR_INVALID, "phase must be 0, 1 or 2");
-  return train_grads_impl(h, stream, params, state, action, futurereward, batch, entropy_beta, workspace,
-                          grads, scalars, phase);
+  if (phase < 0 || phase > 3) return fail(BA3C_ERR_INVALID, "phase must be 0, 1, 2 or 3");
+  if (phase != 3)
+    return train_grads_impl(h, stream, params, state, action, futurereward, batch, entropy_beta, workspace,
+                            grads, scalars, phase);
+  if (h) h->defer_final = true;
+  const int r = train_grads_impl(h, stream, params, state, action, futurereward, batch, entropy_beta,
+                                 workspace, grads, scalars, 0);
+  if (h) h->defer_final = false;
+  return r;
 }
 
 int ba3c_bucket_tensor(const ba3c_handle* h) { return h ? h->idx_fc1 : -1; }
@@ -1429,6 +1466,7 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
     return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  CHECK(flush_reduce(h));
   CHECK(ensure_side_stream(h, s));
   Workspace w = carve(h, workspace, batch, true);
   // no memset of `grads`: the backward pass's single reduction launch writes every element
@@ -1456,6 +1494,7 @@ int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* work
   if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
   if (t0 < 0 || t1 > h->table.n || t0 >= t1) return fail(BA3C_ERR_INVALID, "bad tensor range");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  CHECK(flush_reduce(h));
   float* part = carve(h, workspace, 1, false).sumsq;
   const int c0 = h->table.chunk0[t0], nc = h->table.chunk0[t1] - c0;
   ProbeScope ps(h, s, BA3C_K_CLIP);
@@ -1474,6 +1513,7 @@ int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* work
 int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace) {
   if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  CHECK(flush_reduce(h));
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
   {
     ProbeScope ps(h, s, BA3C_K_CLIP);
@@ -1515,7 +1555,33 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
   a.beta1 = hp->beta1;
   a.beta2 = hp->beta2;
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
-  if (fuse_clip && h->fused_update && h->utag && h->table.nchunks <= h->cus) {
+  const bool fused = fuse_clip && h->fused_update && h->utag && h->table.nchunks <= h->cus;
+  if (fused && h->pend_reduce && h->pend_stream == s && h->pend_grads == grads && chain_ok(h)) {
+    // the pending reduction and this apply as one chained launch: the reduce workgroups
+    // signal, the chunks wait for them before reading their gradient
+    h->pend_reduce = false;
+    const ReduceJobs& jb = h->rjobs;
+    ClipUpdArgs ca{a, h->table, UpdateSync{h->utag, reinterpret_cast<unsigned int*>(h->utag + h->table.nchunks)},
+                   h->spread, CHAIN_SPREAD, (unsigned)jb.blk0[jb.n], h->chain + 4 * CHAIN_SITES};
+    ca.a.clip_part = part;
+    const dim3 gr(jb.blk0[jb.n]), gu(h->table.nchunks);
+    h->merged[BA3C_K_UPDATE] |= 1u << BA3C_K_WGRAD_REDUCE;
+#define BA3C_RCU(O)                                                                                     \
+  launch_chain<false, ReduceJob, ClipUpdJob<O>>(s, CHAIN_REDUCE_UPDATE, 1, 2, 2, jb, gr, ca, gu, 0, dim3(0, 1, 1), h, \
+                                                BA3C_K_UPDATE, true)
+    switch (opt) {
+      case BA3C_OPT_ADAM: return BA3C_RCU(0);
+      case BA3C_OPT_GD: return BA3C_RCU(1);
+      case BA3C_OPT_ADAGRAD: return BA3C_RCU(2);
+      case BA3C_OPT_ADADELTA: return BA3C_RCU(3);
+      case BA3C_OPT_MOMENTUM: return BA3C_RCU(4);
+      case BA3C_OPT_RMS: return BA3C_RCU(5);
+      default: return fail(BA3C_ERR_INVALID, "unknown optimizer id");
+    }
+#undef BA3C_RCU
+  }
+  CHECK(flush_reduce(h));
+  if (fused) {
     a.clip_part = part;
     const dim3 grid(h->table.nchunks);
     const UpdateSync us{h->utag, reinterpret_cast<unsigned int*>(h->utag + h->table.nchunks)};
@@ -1718,6 +1784,7 @@ int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
   if (!h || !flags) return fail(BA3C_ERR_INVALID, "null argument");
   *flags = 0;
+  CHECK(flush_reduce(h));
   if (!h->utag) return BA3C_OK;
   uint32_t e = 0, e2 = 0, e3 = 0;
   HIP_TRY(hipMemcpy(&e, h->utag + h->table.nchunks, sizeof(e), hipMemcpyDeviceToHost));

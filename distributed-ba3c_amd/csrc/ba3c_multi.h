@@ -12,6 +12,7 @@
 #pragma once
 #include "ba3c_band6.h"
 #include "ba3c_gemm6.h"
+#include "ba3c_small.h"
 #include "ba3c_wgrad6.h"
 
 namespace ba3c {
@@ -87,6 +88,38 @@ struct WPrep6Job {
   }
 };
 
+// the pass's weight-gradient reductions, stored for a consumer in the same launch (a chained
+// reduce_clip_update's signalling job)
+struct ReduceJob {
+  using Args = ReduceJobs;
+  static constexpr int LDS = 4 * 64 * 16;
+  __device__ static void run(const Args& a, int x, int, int, int, char* lds, uint32_t*) {
+    wgrad_reduce_body<true>(a, x, lds);
+  }
+};
+
+// the fused clip + optimizer apply as a waiting job: each chunk loads its parameters and
+// slots, then waits for the reduction (zsig: the chain's signal count) before its gradient
+struct ClipUpdArgs {
+  UpdateArgs a;
+  TensorTable tt;
+  UpdateSync us;
+  const unsigned* zsig;   // the chain's spread counters
+  int nctr;
+  unsigned zneed;
+  unsigned* zerr;
+};
+
+template <int OPT>
+struct ClipUpdJob {
+  using Args = ClipUpdArgs;
+  static constexpr int LDS = 32;
+  __device__ static void run(const Args& a, int x, int, int, int gx, char* lds, uint32_t*) {
+    float* f = reinterpret_cast<float*>(lds);
+    clip_update_body<OPT>(a.a, a.tt, a.us, x, gx, a.zsig, a.nctr, a.zneed, a.zerr, f, f + 4);
+  }
+};
+
 // Per job: grid (gx, gy, gz) and the exclusive end of its block range in the launch.
 struct MultiGrid {
   int gx[3], gy[3], end[3];
@@ -138,6 +171,11 @@ struct ChainArgs {
   unsigned* err;    // bit 0: a wait gave up (ba3c_device_errors bit 2)
   int nsig, wmask, nwait;   // nwait: workgroups of the waiting jobs
   int late;                 // waiting jobs that wait inside their body (not before it)
+  // > 0: signalling workgroup b counts into spread counter b % spread (ctr + CHAIN_STRIDE *
+  // that: one 64-byte line each) instead of w[1], so over a thousand signals do not queue on
+  // one address (r05aa: reduce -> clip + update with one counter, +25 us at B=32)
+  unsigned* ctr;
+  int spread;
 };
 
 __device__ __forceinline__ unsigned chain_ld(unsigned* p) {
@@ -152,7 +190,9 @@ __device__ __forceinline__ void multi_chain_body(const typename J0::Args& a0, co
   const int job = b < g.end[0] ? 0 : (b < g.end[1] ? 1 : 2);
   const bool waits = (c.wmask >> job) & 1;
   if (waits && !((c.late >> job) & 1)) {
-    if (threadIdx.x == 0) {
+    if (c.spread) {
+      if (threadIdx.x < 64) chain_wait_spread(c.ctr, c.spread, (unsigned)g.end[c.nsig - 1], c.err);
+    } else if (threadIdx.x == 0) {
       const unsigned need = (unsigned)g.end[c.nsig - 1];
       unsigned spins = 0;
       while (chain_ld(c.w + 1) < need) {
@@ -178,12 +218,16 @@ __device__ __forceinline__ void multi_chain_body(const typename J0::Args& a0, co
   if (job < c.nsig) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(c.w + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(c.spread ? c.ctr + CHAIN_STRIDE * (b % c.spread) : c.w + 1, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   } else if (waits && threadIdx.x == 0) {
     // the last waiter resets the words (every signal was counted before any waiter passed)
     if (__hip_atomic_fetch_add(c.w + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(c.nwait - 1)) {
       __hip_atomic_store(c.w + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c.w + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < c.spread; ++k)
+        __hip_atomic_store(c.ctr + CHAIN_STRIDE * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

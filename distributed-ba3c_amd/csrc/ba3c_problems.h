@@ -71,6 +71,27 @@ __device__ __forceinline__ void chain_wait_wave(const unsigned* sig, unsigned ne
   }
 }
 
+// chained launches' spread signal counters: one per 64-byte line
+constexpr int CHAIN_STRIDE = 16;
+// wave-wide: wait until the `n` (<= 64) spread counters sum to `need` (bounded)
+__device__ __forceinline__ void chain_wait_spread(const unsigned* ctr, int n, unsigned need, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  unsigned spins = 0;
+  while (true) {
+    unsigned v = lane < n ? __hip_atomic_load(const_cast<unsigned*>(ctr) + CHAIN_STRIDE * lane, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (v >= need) break;
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1u << 22)) {
+      if (lane == 0) atomicOr(err, 1u);
+      break;
+    }
+  }
+}
+
 __device__ __forceinline__ void amax_publish(uint32_t* slots, int img, float m, int lane) {
   if (!slots) return;
 #pragma unroll

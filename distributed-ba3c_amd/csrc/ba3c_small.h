@@ -444,21 +444,30 @@ struct ReduceMap {
   float* dst_vb;
 };
 
+// a gradient element; COH: an agent-scope store (global_store sc1), for a consumer in the same
+// launch on another XCD (reduce_clip_update: MI355X's L2s are not coherent)
+template <bool COH = false>
+__device__ __forceinline__ void grad_store(float* p, float v) {
+  if constexpr (COH) st_agent_u32(reinterpret_cast<uint32_t*>(p), __float_as_uint(v));
+  else *p = v;
+}
+
+template <bool COH = false>
 __device__ __forceinline__ void reduce_store(const ReduceMap& mp, int m, int n, float v) {
   if (mp.kind == 0) {
     const int kk = m / mp.cin, c = m - kk * mp.cin;
-    mp.dst[((size_t)kk * mp.cinpad + c) * mp.N + n] = v;
+    grad_store<COH>(mp.dst + ((size_t)kk * mp.cinpad + c) * mp.N + n, v);
   } else if (mp.kind == 1) {
     const int s = n / mp.per, fl = n - s * mp.per;
-    mp.dst[(size_t)s * mp.wstride + (size_t)m * mp.per + fl] = v;  // m == 1600: legacy bias
+    grad_store<COH>(mp.dst + (size_t)s * mp.wstride + (size_t)m * mp.per + fl, v);  // m == 1600: legacy bias
   } else {
     const int F = mp.M - 1;
     if (m < F) {
-      if (n < mp.A) mp.dst[(size_t)m * mp.A + n] = v;
-      else if (n == mp.A) mp.dst_vW[m] = v;
+      if (n < mp.A) grad_store<COH>(mp.dst + (size_t)m * mp.A + n, v);
+      else if (n == mp.A) grad_store<COH>(mp.dst_vW + m, v);
     } else {
-      if (n < mp.A) mp.dst_pib[n] = v;
-      else if (n == mp.A) mp.dst_vb[0] = v;
+      if (n < mp.A) grad_store<COH>(mp.dst_pib + n, v);
+      else if (n == mp.A) grad_store<COH>(mp.dst_vb, v);
     }
   }
 }
@@ -516,10 +525,11 @@ __device__ __forceinline__ int reduce_out_size(const ReduceMap& mp) {
   return mp.kind == 0 ? (mp.M / mp.cin) * mp.cinpad * mp.N : mp.M * mp.N;
 }
 
-__global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs jobs) {
-  __shared__ float red[4][64];
-  __shared__ float4 red4[4][64];
-  const int b = blockIdx.x;
+// workgroup b of the launch; `lds`: 4 KB of scratch (4 x 64 float4)
+template <bool COH>
+__device__ __forceinline__ void wgrad_reduce_body(const ReduceJobs& jobs, int b, char* lds) {
+  float4 (*red4)[64] = reinterpret_cast<float4 (*)[64]>(lds);
+  float (*red)[64] = reinterpret_cast<float (*)[64]>(lds);
   int j = 0;
   while (j + 1 < jobs.n && jobs.blk0[j + 1] <= b) ++j;
   const ReduceMap& mp = jobs.mp[j];
@@ -579,7 +589,14 @@ __global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs 
         const int m = o / mp.N, n = o % mp.N, sidx = n / mp.per, fl = n - sidx * mp.per;
         dst = mp.dst + (size_t)sidx * mp.wstride + (size_t)m * mp.per + fl;
       }
-      *reinterpret_cast<float4*>(dst) = v;
+      if constexpr (COH) {
+        st_agent_u64(reinterpret_cast<unsigned long long*>(dst),
+                     ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x));
+        st_agent_u64(reinterpret_cast<unsigned long long*>(dst) + 1,
+                     ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z));
+      } else {
+        *reinterpret_cast<float4*>(dst) = v;
+      }
     }
     return;
   }
@@ -606,9 +623,14 @@ __global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs 
   __syncthreads();
   if (zg == 0 && o < NO) {
     const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-    if (mp.kind == 0) mp.dst[o] = po >= 0 ? v : 0.f;     // [(kk * cinpad + c) * N + n] == o
-    else reduce_store(mp, o / mp.N, o % mp.N, v);
+    if (mp.kind == 0) grad_store<COH>(mp.dst + o, po >= 0 ? v : 0.f);   // [(kk * cinpad + c) * N + n] == o
+    else reduce_store<COH>(mp, o / mp.N, o % mp.N, v);
   }
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs jobs) {
+  __shared__ float4 red4[4][64];
+  wgrad_reduce_body<false>(jobs, blockIdx.x, reinterpret_cast<char*>(red4));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -834,12 +856,16 @@ __device__ __forceinline__ float wait_partials(const UpdateSync& us, int c0, int
   return ss;
 }
 
+// Chunk b of nblk.  With `zsig` (reduce_clip_update: the gradient is being written by the
+// signalling workgroups of the same launch) the chunk loads its parameters and slots, waits
+// until the nctr spread counters at zsig sum to zneed, then reads its gradient with
+// agent-scope loads.  `red`: 4 floats of LDS, `fsh`: 1.
 template <int OPT>
-__global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, const TensorTable tt,
-                                                          const UpdateSync us) {
-  __shared__ float red[4];
-  __shared__ float fsh;
-  const int b = blockIdx.x;
+__device__ __forceinline__ void clip_update_body(const UpdateArgs& a, const TensorTable& tt,
+                                                 const UpdateSync& us, int b, int nblk,
+                                                 const unsigned* zsig, int nctr, unsigned zneed,
+                                                 unsigned* zerr, float* red, float* fsh_p) {
+  float& fsh = *fsh_p;
   const int lane = threadIdx.x & 63;
   // this launch's generation (issued first: its latency hides behind the data loads)
   const unsigned gen = (unsigned)(ld_agent_u64(us.tag + b) >> 32) + 1u;
@@ -857,10 +883,20 @@ __global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, co
   for (int j = 0; j < PER; ++j) {
     const int i = beg + threadIdx.x + 256 * j;
     const long long k = o + min(i, end - 1);
-    gv[j] = a.g[k];
+    if (!zsig) gv[j] = a.g[k];
     pv[j] = a.p[k];
     s0v[j] = S0 ? a.s0[k] : 0.f;
     s1v[j] = S1 ? a.s1[k] : 0.f;
+  }
+  if (zsig) {
+    if (threadIdx.x < 64) chain_wait_spread(zsig, nctr, zneed, zerr);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const long long k = o + min(beg + (int)threadIdx.x + 256 * j, end - 1);
+      gv[j] = __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(a.g) + k, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+    }
   }
 #pragma unroll
   for (int j = 0; j < PER; ++j)
@@ -881,7 +917,7 @@ __global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, co
     const float sum = wave_sum_f(wait_partials(us, tt.chunk0[t], tt.chunk0[t + 1], gen, lane));
     if (lane == 0) fsh = fminf(rsqrtf(sum) * (float)tt.numel[t], 10.0f);
     if (OPT == 0 && a.dev_powers && b == 0) {
-      (void)wait_partials(us, 0, gridDim.x, gen, lane);   // every chunk has read the powers
+      (void)wait_partials(us, 0, nblk, gen, lane);   // every chunk has read the powers
       if (lane == 0) {
         float* pw = const_cast<float*>(a.dev_powers);
         pw[0] = pw[0] * a.beta1;
@@ -902,6 +938,14 @@ __global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, co
     if constexpr (S1) a.s1[k] = s1;
     a.p[k] = p;
   }
+}
+
+template <int OPT>
+__global__ void __launch_bounds__(256) clip_update_kernel(const UpdateArgs a, const TensorTable tt,
+                                                          const UpdateSync us) {
+  __shared__ float red[4];
+  __shared__ float fsh;
+  clip_update_body<OPT>(a, tt, us, blockIdx.x, gridDim.x, nullptr, 0, 0u, nullptr, red, &fsh);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -149,7 +149,13 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
  * arguments, same workspace) runs conv3..conv0 and finishes the rest.  Phase 0 = both = the
  * bit-identical ba3c_train_grads.  Between the phases the caller may clip and all-reduce the
  * fc1 + heads bucket while the conv layers run (the reference's per-variable PS pushes,
- * OpenAIGym/train.py:598-606). */
+ * OpenAIGym/train.py:598-606).
+ * Phase 3 = phase 0 with the final weight-gradient reduction left pending: the next
+ * ba3c_apply_update(_dev) with fuse_clip on the same handle, stream and `grads` runs it and the
+ * clip + update as ONE chained launch (a launch fewer per step, but measured 4 us slower at
+ * configs[1]: the trainer uses it only with BA3C_DEFER_REDUCE=1); any other entry
+ * point on the handle (forward, train, clip, an unfused or mismatched apply, device_errors)
+ * first launches it on the pass's stream.  `grads` holds the raw gradients only after that. */
 int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                            const int64_t* action, const float* futurereward, int32_t batch,
                            float entropy_beta, void* workspace, float* grads, double* scalars,

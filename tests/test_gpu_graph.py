@@ -334,3 +334,50 @@ def test_chained_launches_match_separate_launches(monkeypatch, B):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(cap.engine.params.cpu().numpy(), plain.engine.params.cpu().numpy())
         assert cap.engine.device_errors() == 0
+
+
+@pytest.mark.parametrize("B,opt", [(32, "adam"), (32, "rms"), (160, "gd")])
+def test_deferred_reduction_rides_on_fused_apply(B, opt):
+    """ba3c_train_grads_phase(phase 3) leaves the pass's weight-gradient reduction pending and
+    the next fused-clip apply runs it as the signalling job of ONE chained launch (reduce ->
+    clip + update).  Against phase 0 + the same apply: the same raw gradients and bit-identical
+    parameters and slots over repeated steps (host and device Adam powers), the reduction
+    reported as merged into the update launch, and no wait gave up.  A phase-3 pass followed
+    by any other call (forward, unfused clip) first launches the pending reduction itself."""
+    from ba3c_amd.engine import Ba3cEngine
+    from ba3c_amd.optimizer import AdamOptimizer, GradientDescentOptimizer, RMSPropOptimizer
+    mk = {"adam": lambda: AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), "rms": lambda: RMSPropOptimizer(1e-3),
+          "gd": lambda: GradientDescentOptimizer(1e-2)}[opt]
+    rs = np.random.RandomState(B + 7)
+    batches = [(torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda(),
+                torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda(),
+                torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()) for _ in range(3)]
+    params = O.init_params(128, 4, 4, seed=11, dtype=np.float32)
+    out = []
+    for phase in (0, 3):
+        eng = Ba3cEngine(num_actions=4, fc_neurons=128, fc_splits=4, max_batch=B)
+        eng.load_params(params)
+        o = mk()
+        if opt == "adam":
+            o.use_device_state(eng.device)
+        got = []
+        for state, action, R in batches:
+            sc = eng.train_grads(state, action, R, phase=phase)
+            o.apply_gradients(eng, fuse_clip=True)
+            got += [sc.clone(), eng.grads.clone(), eng.params.clone()] + [s.clone() for s in o.slots]
+            merged = eng.kernel_merged("update")
+            assert ("wgrad_reduce" in merged) == (phase == 3), merged
+        # phase 3, then calls that are not a fused apply: the pending reduction runs first
+        eng.train_grads(*batches[0], phase=phase)
+        eng.forward(batches[1][0])
+        got.append(eng.grads.clone())
+        eng.train_grads(*batches[1], phase=phase)
+        eng.clip_grads()
+        got.append(eng.grads.clone())
+        torch.cuda.synchronize()
+        assert eng.device_errors() == 0
+        out.append(got)
+        del eng
+    assert len(out[0]) == len(out[1])
+    for i, (a, b) in enumerate(zip(out[0], out[1])):
+        assert torch.equal(a, b), i
