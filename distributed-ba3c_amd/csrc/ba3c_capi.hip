@@ -432,7 +432,7 @@ int launch_reduce(ba3c_handle* h, hipStream_t s, const float* part, int S, const
   const int MN = mp.M * mp.N;
   {
     ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 63) / 64), dim3(256), 0, s, part, S, mp);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((MN + 63) / 64), dim3(64 * RED_G), 0, s, part, S, mp);
   }
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
@@ -846,7 +846,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       h->pend_grads = grads;
     } else if (jb.n > 0) {
       ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
-      hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(256), 0, s, jb);
+      hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(64 * RED_G), 0, s, jb);
     }
     HIP_TRY(hipGetLastError());
     return BA3C_OK;
@@ -1428,7 +1428,7 @@ static int flush_reduce(ba3c_handle* h) {
   h->pend_reduce = false;
   const ReduceJobs& jb = h->rjobs;
   ProbeScope ps(h, h->pend_stream, BA3C_K_WGRAD_REDUCE);
-  hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(256), 0, h->pend_stream, jb);
+  hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(64 * RED_G), 0, h->pend_stream, jb);
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }
@@ -1556,7 +1556,7 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
   a.beta2 = hp->beta2;
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
   const bool fused = fuse_clip && h->fused_update && h->utag && h->table.nchunks <= h->cus;
-  if (fused && h->pend_reduce && h->pend_stream == s && h->pend_grads == grads && chain_ok(h)) {
+  if (RED_G == 4 && fused && h->pend_reduce && h->pend_stream == s && h->pend_grads == grads && chain_ok(h)) {
     // the pending reduction and this apply as one chained launch: the reduce workgroups
     // signal, the chunks wait for them before reading their gradient
     h->pend_reduce = false;

@@ -89,12 +89,13 @@ struct WPrep6Job {
 };
 
 // the pass's weight-gradient reductions, stored for a consumer in the same launch (a chained
-// reduce_clip_update's signalling job)
+// reduce_clip_update's signalling job; 256 threads: the host chains it only when RED_G == 4, so
+// its sums are the plain launch's)
 struct ReduceJob {
   using Args = ReduceJobs;
   static constexpr int LDS = 4 * 64 * 16;
   __device__ static void run(const Args& a, int x, int, int, int, char* lds, uint32_t*) {
-    wgrad_reduce_body<true>(a, x, lds);
+    wgrad_reduce_body<true, 4>(a, x, lds);
   }
 };
 

@@ -472,9 +472,25 @@ __device__ __forceinline__ void reduce_store(const ReduceMap& mp, int m, int n, 
   }
 }
 
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int S,
-                                                           const ReduceMap mp) {
-  __shared__ float red[4][64];
+// Slab groups of the weight-gradient reductions: RED_G groups of 64 lanes (64 RED_G threads per
+// workgroup); group z sums slabs z, z + RED_G, ... in order, then the groups add in order
+#ifndef BA3C_RED_GROUPS
+#define BA3C_RED_GROUPS 4
+#endif
+constexpr int RED_G = BA3C_RED_GROUPS;
+static_assert(RED_G >= 1 && RED_G <= 16, "reduction groups");
+
+template <int NG>
+__device__ __forceinline__ float red_sum(const float (*red)[64], int lane) {
+  float v = red[0][lane];
+#pragma unroll
+  for (int z = 1; z < NG; ++z) v += red[z][lane];
+  return v;
+}
+
+__global__ void __launch_bounds__(64 * RED_G) wgrad_reduce_kernel(const float* __restrict__ part, int S,
+                                                                  const ReduceMap mp) {
+  __shared__ float red[RED_G][64];
   const int lane = threadIdx.x & 63, zg = threadIdx.x >> 6;
   const int MN = mp.M * mp.N;
   const int o = blockIdx.x * 64 + lane;
@@ -482,21 +498,18 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   if (o < MN) {
     int z = zg;
     // 8 slab loads in flight per thread (the adds stay in slab order: deterministic)
-    for (; z + 28 < S; z += 32) {
+    for (; z + 7 * RED_G < S; z += 8 * RED_G) {
       float a[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = part[(size_t)(z + 4 * u) * MN + o];
+      for (int u = 0; u < 8; ++u) a[u] = part[(size_t)(z + RED_G * u) * MN + o];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += a[u];
     }
-    for (; z < S; z += 4) s += part[(size_t)z * MN + o];
+    for (; z < S; z += RED_G) s += part[(size_t)z * MN + o];
   }
   red[zg][lane] = s;
   __syncthreads();
-  if (zg == 0 && o < MN) {
-    const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-    reduce_store(mp, o / mp.N, o % mp.N, v);
-  }
+  if (zg == 0 && o < MN) reduce_store(mp, o / mp.N, o % mp.N, red_sum<RED_G>(red, lane));
 }
 
 // All weight-gradient reductions of one backward pass in ONE launch (one job per layer, each
@@ -525,8 +538,8 @@ __device__ __forceinline__ int reduce_out_size(const ReduceMap& mp) {
   return mp.kind == 0 ? (mp.M / mp.cin) * mp.cinpad * mp.N : mp.M * mp.N;
 }
 
-// workgroup b of the launch; `lds`: 4 KB of scratch (4 x 64 float4)
-template <bool COH>
+// workgroup b of the launch (64 NG threads); `lds`: NG x 64 float4 of scratch
+template <bool COH, int NG>
 __device__ __forceinline__ void wgrad_reduce_body(const ReduceJobs& jobs, int b, char* lds) {
   float4 (*red4)[64] = reinterpret_cast<float4 (*)[64]>(lds);
   float (*red)[64] = reinterpret_cast<float (*)[64]>(lds);
@@ -552,10 +565,10 @@ __device__ __forceinline__ void wgrad_reduce_body(const ReduceJobs& jobs, int b,
       const float4* __restrict__ p4 = reinterpret_cast<const float4*>(part);
       const int MN4 = MN / 4, q = po / 4;
       int z = zg;
-      for (; z + 28 < S; z += 32) {
+      for (; z + 7 * NG < S; z += 8 * NG) {
         float4 a[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a[u] = p4[(size_t)(z + 4 * u) * MN4 + q];
+        for (int u = 0; u < 8; ++u) a[u] = p4[(size_t)(z + NG * u) * MN4 + q];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           sv.x += a[u].x;
@@ -564,7 +577,7 @@ __device__ __forceinline__ void wgrad_reduce_body(const ReduceJobs& jobs, int b,
           sv.w += a[u].w;
         }
       }
-      for (; z < S; z += 4) {
+      for (; z < S; z += NG) {
         const float4 a = p4[(size_t)z * MN4 + q];
         sv.x += a.x;
         sv.y += a.y;
@@ -575,12 +588,15 @@ __device__ __forceinline__ void wgrad_reduce_body(const ReduceJobs& jobs, int b,
     red4[zg][lane] = sv;
     __syncthreads();
     if (zg == 0 && o < NO) {
-      const float4 r0 = red4[0][lane], r1 = red4[1][lane], r2 = red4[2][lane], r3 = red4[3][lane];
-      float4 v;
-      v.x = ((r0.x + r1.x) + r2.x) + r3.x;
-      v.y = ((r0.y + r1.y) + r2.y) + r3.y;
-      v.z = ((r0.z + r1.z) + r2.z) + r3.z;
-      v.w = ((r0.w + r1.w) + r2.w) + r3.w;
+      float4 v = red4[0][lane];
+#pragma unroll
+      for (int z = 1; z < NG; ++z) {
+        const float4 r = red4[z][lane];
+        v.x += r.x;
+        v.y += r.y;
+        v.z += r.z;
+        v.w += r.w;
+      }
       if (po < 0) v = make_float4(0.f, 0.f, 0.f, 0.f);
       float* dst;
       if (mp.kind == 0) {
@@ -610,27 +626,27 @@ __device__ __forceinline__ void wgrad_reduce_body(const ReduceJobs& jobs, int b,
   float s = 0.f;
   if (o < NO && po >= 0) {
     int z = zg;
-    for (; z + 28 < S; z += 32) {
+    for (; z + 7 * NG < S; z += 8 * NG) {
       float a[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = part[(size_t)(z + 4 * u) * MN + po];
+      for (int u = 0; u < 8; ++u) a[u] = part[(size_t)(z + NG * u) * MN + po];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += a[u];
     }
-    for (; z < S; z += 4) s += part[(size_t)z * MN + po];
+    for (; z < S; z += NG) s += part[(size_t)z * MN + po];
   }
   red[zg][lane] = s;
   __syncthreads();
   if (zg == 0 && o < NO) {
-    const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    const float v = red_sum<NG>(red, lane);
     if (mp.kind == 0) grad_store<COH>(mp.dst + o, po >= 0 ? v : 0.f);   // [(kk * cinpad + c) * N + n] == o
     else reduce_store<COH>(mp, o / mp.N, o % mp.N, v);
   }
 }
 
-__global__ void __launch_bounds__(256) wgrad_reduce_all_kernel(const ReduceJobs jobs) {
-  __shared__ float4 red4[4][64];
-  wgrad_reduce_body<false>(jobs, blockIdx.x, reinterpret_cast<char*>(red4));
+__global__ void __launch_bounds__(64 * RED_G) wgrad_reduce_all_kernel(const ReduceJobs jobs) {
+  __shared__ float4 red4[RED_G][64];
+  wgrad_reduce_body<false, RED_G>(jobs, blockIdx.x, reinterpret_cast<char*>(red4));
 }
 
 // ---------------------------------------------------------------------------------------
