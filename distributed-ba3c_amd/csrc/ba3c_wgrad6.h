@@ -687,6 +687,9 @@ __device__ __forceinline__ void wgrad6w_units(const Wg6Args& a, int bx, int gx, 
 #ifndef BA3C_W6W_SPARSE
 #define BA3C_W6W_SPARSE 1
 #endif
+#ifndef BA3C_W6S_HALF
+#define BA3C_W6S_HALF 1       // the band's last 4 quads on a half-size sparse k-step (0: a padded full one)
+#endif
 #ifndef BA3C_DIAG_W6S
 #define BA3C_DIAG_W6S 0       // diagnostics only (A/B timing): 1 = no band staging, 2 = no MFMA loop
 #endif
@@ -922,9 +925,57 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
         }
       }
     };
+    // a band of NQ = 16 SKF + r quads with 0 < r <= 8 ends in a half k-step: the last 8 slots on
+    // v_smfmac_f32_16x16x32_f16 (conv1: 36 quads issue 40 instead of 48)
+    constexpr bool HALF = BA3C_W6S_HALF && G::NQ % 16 != 0 && G::NQ % 16 <= 8;
+    constexpr int SKF = HALF ? G::SKS - 1 : G::SKS;
 #pragma unroll 1
-    for (int s = 0; s + 1 < G::SKS; ++s) kstep(s, std::true_type{});
-    kstep(G::SKS - 1, std::false_type{});
+    for (int s = 0; s + 1 < SKF; ++s) kstep(s, std::true_type{});
+    kstep(SKF - 1, std::false_type{});
+    if constexpr (HALF) {
+      // 16x16x32 lane layouts (scripts/probes/smfmac_probe.hip): group g holds logical K 8g .. 8g + 7
+      // of A and B = the half step's logical quads 2g, 2g + 1 = slots 16 SKF + 2g, + 1 (addr()'s
+      // r = 0, 1 give their pixels)
+      typedef _Float16 f16x4h __attribute__((ext_vector_type(4)));
+      int xh[4];
+      addr(SKF, xh);
+      uint2 ah[2][2];
+      int ixh[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int o = 16 * m + li;
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp)
+          ah[m][sp] = *reinterpret_cast<const uint2*>(yq + ((sp * G::COUT + o) * G::QS + 16 * SKF + 2 * g) * 4);
+        const uint32_t b = *reinterpret_cast<const uint16_t*>(yi + o * G::QS + 16 * SKF + 2 * g);
+        ixh[m] = (int)((b | (b >> 4)) & 0xFFu);
+      }
+      auto read_bh = [&](int u, u32x4 (&bv)[2]) {
+        const int unit = U0 + u, tap = unit / G::CB, cb = unit - tap * G::CB;
+        const int kh = tap / G::KW, kw = tap - kh * G::KW;
+        const int off = (kh * G::WS + kw) * G::PX + cb * 32;
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const uint2 r0 = lds_tr16(xs + xh[0] + off + sp * G::XSB);
+          const uint2 r1 = lds_tr16(xs + xh[1] + off + sp * G::XSB);
+          bv[sp] = u32x4{r0.x, r0.y, r1.x, r1.y};
+        }
+      };
+      u32x4 bh[2][2];                                     // [buffer][plane]
+      read_bh(0, bh[0]);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        if (u + 1 < NU) read_bh(u + 1, bh[(u + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int pr = 0; pr < 3; ++pr)
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+            acc[u][m] = __builtin_amdgcn_smfmac_f32_16x16x32_f16(
+                __builtin_bit_cast(f16x4h, ah[m][pr == 2 ? 1 : 0]), __builtin_bit_cast(f16x8, bh[u & 1][pr == 1 ? 1 : 0]),
+                acc[u][m], ixh[m], 0, 0);
+      }
+    }
   }
 
   // ---- epilogue: C 16x16: lane holds column li = channel 16 cb + li, rows o = 16 m + 4 g + r
