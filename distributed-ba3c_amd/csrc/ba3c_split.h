@@ -145,7 +145,10 @@ struct Conv0S {
   static constexpr int PROWS_W = RB / 2 / 4;       // pooled rows per wave (2)
   static constexpr int MBROW = (WO / 2) / 4;       // m-blocks per pooled row (10)
   static constexpr int MBW = PROWS_W * MBROW;      // m-blocks per wave (20)
-  static constexpr int MCH = 5;                    // m-blocks per accumulator chunk
+#ifndef BA3C_C0F_PIPE
+#define BA3C_C0F_PIPE 1   // chunk c's MFMAs interleaved with chunk c - 1's pool epilogue (two accumulator sets)
+#endif
+  static constexpr int MCH = BA3C_C0F_PIPE ? 2 : 5;  // m-blocks per accumulator chunk
   // prepared weights: [split][nt][kstep][lane] x 16 bytes (room for the 3-plane family)
   static constexpr int WB_U4 = MAXSPLIT * 2 * KSTEPS * 64;
   static_assert(RB % 8 == 0 && HO % RB == 0 && MBW % MCH == 0, "conv0 split geometry");
@@ -414,14 +417,10 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
     if (band + gx < nbands) load_band(band + gx);
     const size_t band_el = (size_t)(img * (G::HO / 2) + y0 / 2) * (G::WO / 2) * G::COUT;
     int bmaxi = 0;                                  // max window-max bits of the band
-#pragma unroll
-    for (int ch = 0; ch < G::MBW / G::MCH; ++ch) {
-      // chunks do not overlap inside a wave (the two waves per SIMD overlap each other's
-      // epilogue and MFMAs): without this fence the scheduler interleaves chunk c + 1's A reads
-      // and MFMAs with chunk c's epilogue, two accumulator sets live -> > 256 registers and one
-      // wave per SIMD (r03g: 0.35 ms)
-      __builtin_amdgcn_sched_barrier(0);
-      f32x4 acc[G::MCH][2];
+    constexpr int NCH = G::MBW / G::MCH, CPR = G::MBROW / G::MCH;   // chunks per band / pooled row
+    static_assert(G::MBROW % G::MCH == 0, "whole chunks per pooled row");
+    // the chunk's MFMAs into `acc`
+    auto chunk_mma = [&](int ch, f32x4 (&acc)[G::MCH][2]) {
 #pragma unroll
       for (int j = 0; j < G::MCH; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -443,6 +442,9 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
             for (int j = 0; j < G::MCH; ++j)
               acc[j][nt] = SP::mfma(af[j], wf[sp][nt][s], acc[j][nt]);
       }
+    };
+    // its pool epilogue, and the copy-out of a completed pooled row
+    auto chunk_epi = [&](int ch, const f32x4 (&acc)[G::MCH][2]) {
       // pool epilogue: lane holds the 4 subs of window 4*mb + lq, channel nt*16 + li.
       // Max of the ReLU'd window = max(v0..v3, +0), taken on the fp32 BITS as signed
       // integers (negative values are negative integers, positive ones order like floats;
@@ -479,9 +481,9 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
           }
         }
       }
-      if (ch % 2 == 1) {
-        // the wave's pooled row 2 wave + ch / 2 is complete in its LDS area: copy it out
-        const size_t row_el = band_el + (size_t)(2 * wave + ch / 2) * (G::WO / 2) * G::COUT;
+      if (ch % CPR == CPR - 1) {
+        // the wave's pooled row 2 wave + ch / CPR is complete in its LDS area: copy it out
+        const size_t row_el = band_el + (size_t)(2 * wave + ch / CPR) * (G::WO / 2) * G::COUT;
         const __amdgpu_buffer_rsrc_t rout = buf_rsrc(a.out + row_el);
         constexpr int NF = (G::WO / 2) * G::COUT * 4 / 16;     // 320 pieces of 16 B
 #pragma unroll
@@ -501,6 +503,32 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
             }
           }
         }
+      }
+    };
+    if constexpr (BA3C_C0F_PIPE) {
+      // software pipeline over the band's chunks: the epilogue of chunk c - 1 (VALU) issues
+      // between the MFMAs of chunk c, which do not depend on it, so one wave keeps the matrix
+      // core and the VALU busy together (two MCH = 2 accumulator sets: 32 registers, fewer than
+      // one MCH = 5 set)
+      f32x4 acc[2][G::MCH][2];
+      chunk_mma(0, acc[0]);
+#pragma unroll
+      for (int ch = 1; ch < NCH; ++ch) {
+        chunk_mma(ch, acc[ch & 1]);
+        chunk_epi(ch - 1, acc[(ch - 1) & 1]);
+      }
+      chunk_epi(NCH - 1, acc[(NCH - 1) & 1]);
+    } else {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        // chunks do not overlap inside a wave (the two waves per SIMD overlap each other's
+        // epilogue and MFMAs): without this fence the scheduler interleaves chunk c + 1's A reads
+        // and MFMAs with chunk c's epilogue, two MCH = 5 accumulator sets live -> > 256
+        // registers and one wave per SIMD (r03g: 0.35 ms)
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 acc[G::MCH][2];
+        chunk_mma(ch, acc);
+        chunk_epi(ch, acc);
       }
     }
     // max over the window maxima, then the scale: a positive scale is monotone in fp32
