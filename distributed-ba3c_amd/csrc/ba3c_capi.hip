@@ -158,6 +158,7 @@ struct ba3c_handle {
   bool pend_reduce = false;
   hipStream_t pend_stream = nullptr;
   const float* pend_grads = nullptr;
+  hipEvent_t ev_pend = nullptr;   // orders a flush on the pass's stream before another stream
   bool defer_final = false;   // set by train_grads_impl for phase 3
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
@@ -1344,6 +1345,7 @@ void ba3c_destroy(ba3c_handle* h) {
   for (auto e : h->ev_fork)
     if (e) (void)hipEventDestroy(e);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->ev_pend) (void)hipEventDestroy(h->ev_pend);
   if (h->side) (void)hipStreamDestroy(h->side);
   if (h->utag) (void)hipFree(h->utag);
   delete h;
@@ -1397,7 +1399,7 @@ size_t ba3c_workspace_size(const ba3c_handle* h, int32_t batch, int32_t train) {
   return carve(h, nullptr, batch, train != 0).bytes;
 }
 
-static int flush_reduce(ba3c_handle* h);
+static int flush_reduce(ba3c_handle* h, hipStream_t s);
 
 int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                  int32_t batch, float explore_factor, void* workspace, float* probs,
@@ -1406,7 +1408,7 @@ int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_
     return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  CHECK(flush_reduce(h));
+  CHECK(flush_reduce(h, s));
   Workspace w = carve(h, workspace, batch, false);
   std::memset(h->merged, 0, sizeof(h->merged));
   int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, false)
@@ -1421,15 +1423,22 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
                             float entropy_beta, void* workspace, float* grads, double* scalars,
                             int32_t phase);
 
-// launch a reduction a phase-3 pass left pending (on its own stream: stream order keeps it
-// ahead of whatever the caller issues after the pass on that stream)
-static int flush_reduce(ba3c_handle* h) {
+// launch a reduction a phase-3 pass left pending, on the pass's stream; a call on another
+// stream `s` then waits for it (an event recorded by the caller after the pass predates it)
+static int flush_reduce(ba3c_handle* h, hipStream_t s) {
   if (!h || !h->pend_reduce) return BA3C_OK;
   h->pend_reduce = false;
   const ReduceJobs& jb = h->rjobs;
-  ProbeScope ps(h, h->pend_stream, BA3C_K_WGRAD_REDUCE);
-  hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(64 * RED_G), 0, h->pend_stream, jb);
+  {
+    ProbeScope ps(h, h->pend_stream, BA3C_K_WGRAD_REDUCE);
+    hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(64 * RED_G), 0, h->pend_stream, jb);
+  }
   HIP_TRY(hipGetLastError());
+  if (s != h->pend_stream) {
+    if (!h->ev_pend) HIP_TRY(hipEventCreateWithFlags(&h->ev_pend, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(h->ev_pend, h->pend_stream));
+    HIP_TRY(hipStreamWaitEvent(s, h->ev_pend, 0));
+  }
   return BA3C_OK;
 }
 
@@ -1466,7 +1475,7 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
     return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  CHECK(flush_reduce(h));
+  CHECK(flush_reduce(h, s));
   CHECK(ensure_side_stream(h, s));
   Workspace w = carve(h, workspace, batch, true);
   // no memset of `grads`: the backward pass's single reduction launch writes every element
@@ -1494,7 +1503,7 @@ int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* work
   if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
   if (t0 < 0 || t1 > h->table.n || t0 >= t1) return fail(BA3C_ERR_INVALID, "bad tensor range");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  CHECK(flush_reduce(h));
+  CHECK(flush_reduce(h, s));
   float* part = carve(h, workspace, 1, false).sumsq;
   const int c0 = h->table.chunk0[t0], nc = h->table.chunk0[t1] - c0;
   ProbeScope ps(h, s, BA3C_K_CLIP);
@@ -1513,7 +1522,7 @@ int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* work
 int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace) {
   if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  CHECK(flush_reduce(h));
+  CHECK(flush_reduce(h, s));
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
   {
     ProbeScope ps(h, s, BA3C_K_CLIP);
@@ -1580,7 +1589,7 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
     }
 #undef BA3C_RCU
   }
-  CHECK(flush_reduce(h));
+  CHECK(flush_reduce(h, s));
   if (fused) {
     a.clip_part = part;
     const dim3 grid(h->table.nchunks);
@@ -1784,7 +1793,7 @@ int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
   if (!h || !flags) return fail(BA3C_ERR_INVALID, "null argument");
   *flags = 0;
-  CHECK(flush_reduce(h));
+  CHECK(flush_reduce(h, h->pend_stream));   // (the copies below synchronise the device)
   if (!h->utag) return BA3C_OK;
   uint32_t e = 0, e2 = 0, e3 = 0;
   HIP_TRY(hipMemcpy(&e, h->utag + h->table.nchunks, sizeof(e), hipMemcpyDeviceToHost));

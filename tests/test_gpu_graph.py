@@ -343,7 +343,8 @@ def test_deferred_reduction_rides_on_fused_apply(B, opt):
     clip + update).  Against phase 0 + the same apply: the same raw gradients and bit-identical
     parameters and slots over repeated steps (host and device Adam powers), the reduction
     reported as merged into the update launch, and no wait gave up.  A phase-3 pass followed
-    by any other call (forward, unfused clip) first launches the pending reduction itself."""
+    by any other call (forward, unfused clip — also on another stream) first launches the
+    pending reduction itself."""
     from ba3c_amd.engine import Ba3cEngine
     from ba3c_amd.optimizer import AdamOptimizer, GradientDescentOptimizer, RMSPropOptimizer
     mk = {"adam": lambda: AdamOptimizer(1e-3, 0.8, 0.75, 1e-8), "rms": lambda: RMSPropOptimizer(1e-3),
@@ -373,6 +374,15 @@ def test_deferred_reduction_rides_on_fused_apply(B, opt):
         got.append(eng.grads.clone())
         eng.train_grads(*batches[1], phase=phase)
         eng.clip_grads()
+        got.append(eng.grads.clone())
+        # a call on another stream ordered after the pass by the caller's own event (recorded
+        # before the pending reduction was launched) still sees the reduced gradient
+        eng.train_grads(*batches[2], phase=phase)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            eng.clip_grads()
+        torch.cuda.current_stream().wait_stream(side)
         got.append(eng.grads.clone())
         torch.cuda.synchronize()
         assert eng.device_errors() == 0
