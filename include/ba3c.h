@@ -3,9 +3,10 @@
  *
  * Plain pointers and sizes only: every data buffer is owned by the caller (the Python
  * host allocates them with PyTorch-ROCm); the handle owns static configuration, a few HIP
- * events and 16 bytes of device memory allocated by ba3c_create (the grid-barrier words of
- * the fused clip + optimizer launch; without a device they stay unallocated and the apply
- * uses two launches).  One handle serves one stream at a time.  No other call allocates
+ * events and a few KB of device memory allocated by ba3c_create (the tagged-partial words of
+ * the fused clip + optimizer launch and of the one-launch bucket clip, the chained launches'
+ * signal counters; without a device they stay unallocated and those launches fall back to
+ * unchained ones).  One handle serves one stream at a time.  No other call allocates
  * device memory, none synchronises the stream except ba3c_probe_read, and none throws:
  * every entry returns a BA3C_* status and
  * ba3c_last_error() holds a thread-local message.  All device pointers must be 16-byte
@@ -155,7 +156,7 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
  * clip + update as ONE chained launch (a launch fewer per step, but measured 4 us slower at
  * configs[1]: the trainer uses it only with BA3C_DEFER_REDUCE=1); any other entry
  * point on the handle (forward, train, clip, an unfused or mismatched apply, device_errors)
- * first launches it on the pass's stream.  `grads` holds the raw gradients only after that. */
+ * first launches it on the pass's stream (a call on another stream then waits for it).  `grads` holds the raw gradients only after that. */
 int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                            const int64_t* action, const float* futurereward, int32_t batch,
                            float entropy_beta, void* workspace, float* grads, double* scalars,
