@@ -148,7 +148,10 @@ struct Conv0S {
 #ifndef BA3C_C0F_PIPE
 #define BA3C_C0F_PIPE 1   // chunk c's MFMAs interleaved with chunk c - 1's pool epilogue (two accumulator sets)
 #endif
-  static constexpr int MCH = BA3C_C0F_PIPE ? 2 : 5;  // m-blocks per accumulator chunk
+#ifndef BA3C_C0F_MCH
+#define BA3C_C0F_MCH (BA3C_C0F_PIPE ? 2 : 5)
+#endif
+  static constexpr int MCH = BA3C_C0F_MCH;          // m-blocks per accumulator chunk
   // prepared weights: [split][nt][kstep][lane] x 16 bytes (room for the 3-plane family)
   static constexpr int WB_U4 = MAXSPLIT * 2 * KSTEPS * 64;
   static_assert(RB % 8 == 0 && HO % RB == 0 && MBW % MCH == 0, "conv0 split geometry");
