@@ -149,7 +149,9 @@ class Ba3cEngine(object):
         """Forward + loss + backward; raw gradients into `grads` (default self.grads).
         Returns the device float64 scalars tensor (order: _lib.SCALAR_NAMES).  phase 1 / 2
         split the pass at the fc1 + heads bucket (ba3c_train_grads_phase); phase 3 leaves the
-        final gradient reduction to the next fused-clip apply_update (one launch fewer)."""
+        final gradient reduction to the next fused-clip apply_update (one launch fewer): until
+        then `grads` holds unreduced data for any reader outside this handle — call
+        flush_pending() before reading it through torch."""
         B = self._check_state(state)
         assert action.dtype == torch.int64 and action.shape == (B,) and action.is_cuda
         assert futurereward.dtype == torch.float32 and futurereward.shape == (B,)
@@ -160,6 +162,10 @@ class Ba3cEngine(object):
                                                    float(entropy_beta), _ptr(self._workspace(True)),
                                                    _ptr(grads), _ptr(self.scalars), int(phase)))
         return self.scalars
+
+    def flush_pending(self):
+        """Launch a weight-gradient reduction a phase-3 pass left pending (no-op otherwise)."""
+        _lib.check(self.lib.ba3c_flush_pending(self.h))
 
     def bucket_split(self):
         """(first tensor, flat offset) of the fc1 + heads gradient bucket."""

@@ -408,7 +408,7 @@ class SyncReplicasOptimizer(object):
                 return None
             self._rccl = comm
             import atexit
-            atexit.register(self.close)
+            atexit.register(self._close_at_exit)
         return self._rccl
 
     def rccl_info(self):
@@ -416,11 +416,21 @@ class SyncReplicasOptimizer(object):
         return self._rccl.info() if self._rccl else None
 
     def close(self):
-        """Destroy the direct RCCL communicator (before dist.destroy_process_group; also run at
-        interpreter exit), so no RCCL proxy thread outlives the process group."""
+        """Destroy the direct RCCL communicator (before dist.destroy_process_group), so no
+        RCCL proxy thread outlives the process group.  Waits for the device first: call it
+        only when every rank reached the same point (bench.py does, after a barrier)."""
         if self._rccl:
             torch.cuda.synchronize(self._rccl.device)
             self._rccl.close()
+            self._rccl = None
+
+    def _close_at_exit(self):
+        """Interpreter exit without an explicit close() (train.py, torchrun, a rank leaving on
+        an exception): abort the communicator instead of synchronising, since an all-reduce
+        still waiting on a dead or diverged peer would never finish and the rank would hang
+        at exit instead of failing."""
+        if self._rccl:
+            self._rccl.close(abort=True)
             self._rccl = None
 
     # HIP event recorded on the exchange stream after the last asynchronous bucket sum of the

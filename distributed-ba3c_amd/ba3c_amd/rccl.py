@@ -44,6 +44,7 @@ def _lib():
         lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        lib.ncclCommAbort.argtypes = [ctypes.c_void_p]
         for fn in ("ncclCommCount", "ncclCommCuDevice", "ncclCommUserRank"):
             getattr(lib, fn).argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         lib.ncclGetVersion.argtypes = [ctypes.POINTER(ctypes.c_int)]
@@ -125,7 +126,10 @@ class RcclComm(object):
         _check(_lib().ncclAllReduce(p, p, buf.numel(), NCCL_FLOAT32, NCCL_SUM, self._comm,
                                     ctypes.c_void_p(stream.cuda_stream)), "ncclAllReduce")
 
-    def close(self):
+    def close(self, abort=False):
+        """ncclCommDestroy (the caller has synchronised the device), or with `abort`
+        ncclCommAbort, which does not wait for collectives still enqueued (exit paths: a peer
+        may be dead, so outstanding work may never finish)."""
         if self._comm:
-            _lib().ncclCommDestroy(self._comm)
+            (_lib().ncclCommAbort if abort else _lib().ncclCommDestroy)(self._comm)
             self._comm = ctypes.c_void_p()

@@ -83,7 +83,10 @@ class Ba3cTrainer(object):
         # fused apply's launch (ba3c_train_grads_phase phase 3: one launch fewer).  Default off:
         # same-box r05ab, B=32 step 0.1607 -> 0.1646 ms, B=2048 1.743 -> 1.752 ms (the hand-off's
         # agent-scope stores / loads and signal counters cost more than the launch boundary)
-        self._defer_reduce = os.environ.get("BA3C_DEFER_REDUCE", "0") == "1"
+        flag = os.environ.get("BA3C_DEFER_REDUCE", "0")
+        if flag not in ("0", "1"):
+            raise ValueError("BA3C_DEFER_REDUCE must be 0 or 1 (got %r)" % flag)
+        self._defer_reduce = flag == "1"
         if isinstance(self.optimizer, SyncReplicasOptimizer):
             self.optimizer.broadcast_variables(self.engine)
 

@@ -1466,6 +1466,11 @@ int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, co
 
 int ba3c_bucket_tensor(const ba3c_handle* h) { return h ? h->idx_fc1 : -1; }
 
+int ba3c_flush_pending(ba3c_handle* h) {
+  if (!h) return fail(BA3C_ERR_INVALID, "null handle");
+  return flush_reduce(h, h->pend_stream);
+}
+
 static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                             const int64_t* action, const float* futurereward, int32_t batch,
                             float entropy_beta, void* workspace, float* grads, double* scalars,
@@ -1543,6 +1548,9 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
   if ((need0 && !check_ptr(slot0)) || (need1 && !check_ptr(slot1)))
     return fail(BA3C_ERR_INVALID, "missing optimizer slot");
   if (fuse_clip && !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "fuse_clip needs a workspace");
+  // validated before anything is launched or the pending reduction is consumed (ADVICE r05:
+  // the chained branch below clears pend_reduce, so an unknown id there would drop it)
+  if (opt < BA3C_OPT_ADAM || opt > BA3C_OPT_RMS) return fail(BA3C_ERR_INVALID, "unknown optimizer id");
   hipStream_t s = static_cast<hipStream_t>(stream);
   UpdateArgs a{};
   a.p = params;
@@ -1793,12 +1801,23 @@ int ba3c_kernel_family(const ba3c_handle* h, int32_t kid) {
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
   if (!h || !flags) return fail(BA3C_ERR_INVALID, "null argument");
   *flags = 0;
-  CHECK(flush_reduce(h, h->pend_stream));   // (the copies below synchronise the device)
+  CHECK(flush_reduce(h, h->pend_stream));
   if (!h->utag) return BA3C_OK;
+  // every stream, the non-blocking ones torch creates included (a null-stream copy does not
+  // wait for those)
+  HIP_TRY(hipDeviceSynchronize());
   uint32_t e = 0, e2 = 0, e3 = 0;
   HIP_TRY(hipMemcpy(&e, h->utag + h->table.nchunks, sizeof(e), hipMemcpyDeviceToHost));
   if (h->ctag) HIP_TRY(hipMemcpy(&e2, h->ctag + h->table.nchunks, sizeof(e2), hipMemcpyDeviceToHost));
   if (h->chain) HIP_TRY(hipMemcpy(&e3, h->chain + 4 * CHAIN_SITES, sizeof(e3), hipMemcpyDeviceToHost));
+  if (e3 && h->chain_on) {
+    // a chained wait gave up: a late signal may have landed after the last waiter reset the
+    // site's words, so they can no longer be trusted.  Zero them from the host and stop
+    // chaining on this handle (the error bit stays set)
+    h->chain_on = false;
+    HIP_TRY(hipMemset(h->chain, 0, 4 * CHAIN_SITES * sizeof(unsigned)));
+    HIP_TRY(hipMemset(h->spread, 0, CHAIN_SPREAD * CHAIN_STRIDE * sizeof(unsigned)));
+  }
   *flags = e | (e2 << 1) | (e3 << 2);
   return BA3C_OK;
 }

@@ -161,6 +161,10 @@ int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, co
                            const int64_t* action, const float* futurereward, int32_t batch,
                            float entropy_beta, void* workspace, float* grads, double* scalars,
                            int32_t phase);
+/* Launch a reduction that a phase-3 pass left pending, on the pass's stream (no-op when none
+ * is pending).  For callers that read `grads` through another API (a torch view, a gradient
+ * summary) between the pass and the fused apply. */
+int ba3c_flush_pending(ba3c_handle* h);
 /* First tensor of the fc1 + heads bucket (tensors before it: the conv layers). */
 int ba3c_bucket_tensor(const ba3c_handle* h);
 
@@ -210,7 +214,8 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
  * bit 1: a one-launch ba3c_clip_grads_range, stopped waiting for another workgroup's partial;
  * bit 2: a chained launch's conv0 workgroups stopped waiting for the zeroing of the ReLU
  * counters / max slots — the results are invalid).  0 in normal operation.  Synchronises the
- * device (diagnostics / tests only). */
+ * device (diagnostics / tests only).  Once bit 2 is seen the handle zeroes its chain words and
+ * stops chaining launches (the flag stays set). */
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags);
 
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
