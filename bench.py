@@ -317,7 +317,43 @@ PHASE2_KERNELS = ("conv3_dgrad", "conv3_wgrad", "conv2_dgrad", "conv1_dgrad", "c
                   "wgrad_reduce")
 
 
-def exchange_report(tr, batch, timeline, iters, world):
+def occupy_table(tr, batch, ks, window_us, phase2_us, iters, world, probe, base):
+    """--occupy: for each K, a launch on the exchange stream holds K CUs (ba3c_occupy_cus)
+    right after the fc1 + heads bucket's sum, first for `window_us` (about the bucket's sum on
+    an 8-GPU node) then for the whole of phase 2 (`phase2_us`, the worst case: CUs missing
+    during every phase-2 launch).  Each row: the step time over `iters` steps and every
+    phase-2 launch's time, against `base` (the same launches with the exchange running and no
+    occupier) — `ideal` is what a perfectly balanced launch would take with K of the CUs gone
+    for its whole length (base x CUs / (CUs - K)); a static per-CU partition of work instead
+    waits for the occupier before its displaced workgroups start."""
+    opt = tr.optimizer
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    rows = []
+    try:
+        for k in ks:
+            for mode, us in (("window", window_us), ("phase2", phase2_us)):
+                opt.occupy = (k, us)
+                sync_all(world)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                ev[0].record()
+                for _ in range(iters):
+                    tr.train_step(*batch)
+                ev[1].record()
+                sync_all(world)
+                step = ev[0].elapsed_time(ev[1]) / iters
+                launches = {kk: probe(kk) for kk in PHASE2_KERNELS}
+                rows.append({"cus_held": k, "mode": mode, "hold_us": round(us, 1),
+                             "step_ms": round(step, 4),
+                             "launch_ms": {kk: round(v, 4) for kk, v in launches.items()},
+                             "slowdown": {kk: round(v / base[kk], 3) if base.get(kk) else None
+                                          for kk, v in launches.items()},
+                             "ideal_slowdown_full_overlap": round(cus / (cus - k), 3)})
+    finally:
+        opt.occupy = None
+    return rows
+
+
+def exchange_report(tr, batch, timeline, iters, world, occupy=(), occupy_us=50.0):
     """N > 1 (or --sync-path): where the data-parallel exchange's time goes.  `timeline` holds
     the HIP events the timed steps recorded inside the real bucketed step (ExchangeTimeline:
     phase 1, phase 2, each bucket's all-reduce from its clip to its end on the exchange
@@ -362,6 +398,11 @@ def exchange_report(tr, batch, timeline, iters, world):
     el = el.tolist()
     tl.update({k: round(v, 4) for k, v in zip(names, el[:len(names)])})
     n = len(PHASE2_KERNELS)
+    occ = None
+    if occupy:
+        base = dict(zip(PHASE2_KERNELS, el[len(names):len(names) + n]))
+        occ = occupy_table(tr, batch, occupy, occupy_us, tl["phase2_ms"] * 1000.0, iters, world,
+                           probe, base)
     return {"buckets": {"fc1_heads": {"bytes": 4 * (total - off)}, "conv": {"bytes": 4 * off}},
             "backend": dist.get_backend() if dist.is_initialized() else None,
             # bucket sums through RCCL driven directly (rccl.py) or torch's collective
@@ -371,6 +412,7 @@ def exchange_report(tr, batch, timeline, iters, world):
                                  for k, a, b in zip(PHASE2_KERNELS, el[len(names):len(names) + n],
                                                     el[len(names) + n:])},
             "probe_iters": iters,
+            "occupy": occ,
             # what RCCL itself reports on every rank (rank count, own rank, HIP device, PCI
             # bus id): world ranks on world distinct devices
             "rccl_comms": rccl_comms}
@@ -535,6 +577,13 @@ def main():
     ap.add_argument("--sync-path", action="store_true",
                     help="N=1: run the N>1 step (SyncReplicasOptimizer: phase-split backward, "
                          "per-bucket clip, unfused update) in a world-1 RCCL group")
+    ap.add_argument("--occupy", default="",
+                    help="with --sync-path or N>1: comma-separated CU counts K; for each, a launch "
+                         "on the exchange stream holds K CUs after the fc1 bucket's sum (for "
+                         "--occupy-us, and for the whole of phase 2) and the line's "
+                         "exchange.occupy table reports the step and every phase-2 launch")
+    ap.add_argument("--occupy-us", type=float, default=50.0,
+                    help="the short occupancy window (microseconds) of --occupy")
     ap.add_argument("--exchange-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -654,7 +703,9 @@ def run_rank(args, world, rank, local):
 
     rc = health(out, flags, identical)
     if sync:
-        out["exchange"] = exchange_report(tr, batch, timeline, max(args.steps // 3, 5), world)
+        ks = [int(k) for k in args.occupy.split(",") if k.strip()]
+        out["exchange"] = exchange_report(tr, batch, timeline, max(args.steps // 3, 5), world,
+                                          ks, args.occupy_us)
     if not args.no_overlap:
         out["overlap"] = overlap_bench(tr, batch, args.predict_batch, 10, world)
     if not args.no_b32:

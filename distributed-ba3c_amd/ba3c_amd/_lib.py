@@ -75,6 +75,7 @@ def load():
         "ba3c_train_grads_phase": (i32, [P, P, P, P, P, P, i32, f32, P, P, P, i32]),
         "ba3c_bucket_tensor": (i32, [P]),
         "ba3c_flush_pending": (i32, [P]),
+        "ba3c_occupy_cus": (i32, [P, i32, ctypes.c_double]),
         "ba3c_apply_update": (i32, [P, P, i32, P, P, P, P, ctypes.POINTER(Ba3cOptParams), f32,
                                     i32, P]),
         "ba3c_apply_update_dev": (i32, [P, P, i32, P, P, P, P, ctypes.POINTER(Ba3cOptParams), P,

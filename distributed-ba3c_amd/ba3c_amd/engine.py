@@ -167,6 +167,11 @@ class Ba3cEngine(object):
         """Launch a weight-gradient reduction a phase-3 pass left pending (no-op otherwise)."""
         _lib.check(self.lib.ba3c_flush_pending(self.h))
 
+    def occupy_cus(self, stream, n_cus, usec):
+        """Diagnostic: hold `n_cus` CUs for `usec` microseconds on torch stream `stream`."""
+        _lib.check(self.lib.ba3c_occupy_cus(ctypes.c_void_p(stream.cuda_stream), int(n_cus),
+                                            float(usec)))
+
     def bucket_split(self):
         """(first tensor, flat offset) of the fc1 + heads gradient bucket."""
         t = int(self.lib.ba3c_bucket_tensor(self.h))

@@ -479,6 +479,7 @@ class SyncReplicasOptimizer(object):
                 return _StagedWork(work, host, buf, stream=comm, end=end)
             if rccl is not None:
                 rccl.all_reduce_sum(buf, comm)
+                self._occupy(engine, comm)
                 if self._ar_event is None:
                     self._ar_event = torch.cuda.Event()
                 self._ar_event.record(comm)
@@ -486,9 +487,19 @@ class SyncReplicasOptimizer(object):
             else:
                 work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                 work.wait()                   # `comm` waits for the collective's stream
+                self._occupy(engine, comm)
             if end is not None:
                 end.record(comm)
         return _StreamJoin(comm)
+
+    # bench.py --occupy: (K, microseconds) — after the fc1 + heads bucket's sum, a launch on the
+    # exchange stream holds K CUs for that long (ba3c_occupy_cus), standing in for the CUs
+    # RCCL's channel workgroups take on a multi-GPU node while phase 2 runs.  None: off.
+    occupy = None
+
+    def _occupy(self, engine, stream):
+        if self.occupy:
+            engine.occupy_cus(stream, *self.occupy)
 
     def apply_gradients(self, engine):
         self._opt.apply_gradients(engine, grad_scale=1.0 / self.replicas_to_aggregate,

@@ -1822,6 +1822,16 @@ int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
   return BA3C_OK;
 }
 
+int ba3c_occupy_cus(void* stream, int32_t n_cus, double usec) {
+  if (n_cus < 0 || n_cus > 4096 || !(usec >= 0.0) || usec > 1e6)
+    return fail(BA3C_ERR_INVALID, "n_cus in [0, 4096], usec in [0, 1e6]");
+  if (n_cus == 0 || usec == 0.0) return BA3C_OK;
+  hipLaunchKernelGGL(occupy_kernel, dim3(n_cus), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     (unsigned long long)(usec * 100.0));   // 100 MHz realtime clock
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches) {
   if (!h) return fail(BA3C_ERR_INVALID, "null handle");
   for (int i = 0; i < h->probe_used; ++i) {

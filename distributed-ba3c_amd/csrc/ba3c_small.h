@@ -1018,6 +1018,21 @@ __global__ void __launch_bounds__(256) clip_range_kernel(float* __restrict__ g, 
 // a = searchsorted(cdf, u, 'right').  flag bits: 1 non-finite p (train.py:381), 2 |sum-1| >
 // sqrt(eps_f32) ("probabilities do not sum to 1"), 4 negative p.
 // ---------------------------------------------------------------------------------------
+// Diagnostic (ba3c_occupy_cus): each workgroup declares the whole 160 KiB of a CU's LDS, so
+// `n` workgroups hold `n` distinct CUs against every kernel that uses LDS (all the conv
+// kernels) for `ticks` of the 100 MHz realtime clock — a stand-in for RCCL's channel
+// workgroups sharing the chip with the persistent conv kernels during a bucket's all-reduce
+// (bench.py --occupy).  No memory traffic; the spin sleeps between clock reads.
+__global__ void __launch_bounds__(64) occupy_kernel(unsigned long long ticks) {
+  __shared__ uint4 hold[163840 / 16];
+  hold[threadIdx.x] = make_uint4(threadIdx.x, 0u, 0u, 0u);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+  __syncthreads();
+  const unsigned v = hold[(threadIdx.x + 1) & 63].x;
+  asm volatile("" ::"v"(v));   // keeps the LDS declaration (and so the CU) allocated
+}
+
 __global__ void __launch_bounds__(256) sample_kernel(const float* __restrict__ probs,
                                                      const double* __restrict__ u, int B, int A,
                                                      int64_t* __restrict__ actions, int* flag) {

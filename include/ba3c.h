@@ -219,6 +219,12 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags);
 
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
+/* Diagnostic, not part of the reference's interface: enqueue on `stream` a launch of `n_cus`
+ * workgroups that each hold one whole CU (all 160 KiB of its LDS) for `usec` microseconds,
+ * doing nothing.  bench.py --occupy uses it on the exchange stream to stand in for RCCL's
+ * channel workgroups while the conv backward runs (how persistent kernels degrade when K CUs
+ * are missing). */
+int ba3c_occupy_cus(void* stream, int32_t n_cus, double usec);
 
 /* Arithmetic path of kernel `kernel_id` on this handle (for roofline accounting; no
  * reference counterpart): the number of 16-bit MFMA products it issues per fp32 product —
