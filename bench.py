@@ -28,6 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "distributed-ba3c_amd"))
 sys.path.insert(0, ROOT)
 
+from ba3c_amd import hipevent  # noqa: E402  (HIP events without a system fence)
+
 METRIC = "BA3C train-step samples/sec, 84x84x4 frames, batch 32 & 2048, at 1/2/4/8 GPUs"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (spec)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (16 x the fp32 rate)
@@ -230,7 +232,7 @@ def time_steps(tr, batch, steps, warmup, world, probe=None):
     sync_all(world)
     if probe is not None:
         tr.engine.probe_enable(probe)   # bracket the dominant kernel over the timed steps only
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    evs = [hipevent.timing_event() for _ in range(steps + 1)]   # no system fence (hipevent.py)
     t0 = time.perf_counter()
     evs[0].record()
     for i in range(steps):
@@ -286,16 +288,19 @@ def overlap_bench(tr, batch, pred_batch, iters, world):
             if mode in ("train", "both"):
                 if mode == "both":
                     pe.params.copy_(eng.params)          # snapshot on the learner stream
-                    ev = torch.cuda.Event()
+                    ev = hipevent.join_event()
                     ev.record(main)
                 tr.train_step(*batch)
             if mode == "pred":
                 pred_only()
             if mode == "both":
-                ps.wait_event(ev)
+                if isinstance(ev, hipevent.HipEvent):
+                    ev.wait(ps)
+                else:
+                    ps.wait_event(ev)
                 with torch.cuda.stream(ps):
                     pe.forward(states)
-                main.wait_stream(ps)
+                hipevent.wait_stream(main, ps)
         sync_all(world)
         return (time.perf_counter() - t0) / n * 1000.0
 
@@ -334,7 +339,7 @@ def occupy_table(tr, batch, ks, window_us, phase2_us, iters, world, probe, base)
             for mode, us in (("window", window_us), ("phase2", phase2_us)):
                 opt.occupy = (k, us)
                 sync_all(world)
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                ev = [hipevent.timing_event() for _ in range(2)]
                 ev[0].record()
                 for _ in range(iters):
                     tr.train_step(*batch)

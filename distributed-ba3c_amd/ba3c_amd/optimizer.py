@@ -14,6 +14,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import hipevent
+
 _f = np.float32
 
 
@@ -193,7 +195,7 @@ class _StagedWork(object):
             self.dst.copy_(self.host)
             if self.end is not None:
                 self.end.record(self.stream)
-        torch.cuda.current_stream(self.dst.device).wait_stream(self.stream)
+        hipevent.wait_stream(torch.cuda.current_stream(self.dst.device), self.stream)
         return True
 
 
@@ -203,9 +205,12 @@ class _StreamJoin(object):
 
     def __init__(self, stream):
         self.stream = stream
+        self.joined = False      # set once the current stream already waits for the sum
 
     def wait(self):
-        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+        if not self.joined:
+            hipevent.wait_stream(torch.cuda.current_stream(self.stream.device), self.stream)
+            self.joined = True
         return True
 
 
@@ -353,9 +358,17 @@ class SyncReplicasOptimizer(object):
     def comm_stream(self, device):
         """The exchange stream of the bucketed step: each bucket's sum is issued on it after
         the bucket's clip, so its start and end can be marked with HIP events in the same
-        stream order as the collective (torch's NCCL stream joins it on wait())."""
+        stream order as the collective (torch's NCCL stream joins it on wait()).
+
+        High priority by default (BA3C_XCHG_PRIORITY=0: normal): the backward's persistent conv
+        kernels fill every CU, so the collective's workgroups can only start at a kernel
+        boundary, and there the dispatcher should place them ahead of the next conv kernel's
+        workgroups rather than after all of them."""
         if self._comm is None:
-            self._comm = torch.cuda.Stream(device=device)
+            flag = os.environ.get("BA3C_XCHG_PRIORITY", "1")
+            if flag not in ("0", "1"):
+                raise ValueError("BA3C_XCHG_PRIORITY must be 0 or 1 (got %r)" % flag)
+            self._comm = torch.cuda.Stream(device=device, priority=-1 if flag == "1" else 0)
         return self._comm
 
     # RCCL driven directly (rccl.py) for the bucket sums on a 'nccl' group; BA3C_DIRECT_RCCL=0
@@ -439,6 +452,8 @@ class SyncReplicasOptimizer(object):
     # serialisation
     _ar_done = None
     _ar_event = None
+    _ready_event = None
+    _fc1_join = None
 
     def aggregate_bucket_async(self, engine, t0, t1, off0, off1, marks=None, last=False):
         """Clip tensors [t0, t1) and start the RCCL sum of flat range [off0, off1); returns
@@ -460,8 +475,16 @@ class SyncReplicasOptimizer(object):
         rccl = self.direct_rccl(buf.device)
         if rccl is not None and last:
             if self._ar_done is not None:
-                cur.wait_event(self._ar_done)     # the exchange stream's sum is enqueued first
+                # the exchange stream's sum is enqueued first; this wait also joins it, so the
+                # update needs no second cross-stream wait
+                if isinstance(self._ar_done, hipevent.HipEvent):
+                    self._ar_done.wait(cur)
+                else:
+                    cur.wait_event(self._ar_done)
                 self._ar_done = None
+                if self._fc1_join is not None:
+                    self._fc1_join.joined = True
+                    self._fc1_join = None
             if begin is not None:
                 begin.record(cur)
             rccl.all_reduce_sum(buf, cur)
@@ -469,7 +492,9 @@ class SyncReplicasOptimizer(object):
                 end.record(cur)
             return None
         comm = self.comm_stream(buf.device)
-        comm.wait_stream(cur)
+        if self._ready_event is None:
+            self._ready_event = hipevent.join_event()
+        hipevent.wait_stream(comm, cur, self._ready_event)
         with torch.cuda.stream(comm):
             if begin is not None:
                 begin.record(comm)
@@ -481,7 +506,7 @@ class SyncReplicasOptimizer(object):
                 rccl.all_reduce_sum(buf, comm)
                 self._occupy(engine, comm)
                 if self._ar_event is None:
-                    self._ar_event = torch.cuda.Event()
+                    self._ar_event = hipevent.join_event()
                 self._ar_event.record(comm)
                 self._ar_done = self._ar_event
             else:
@@ -490,7 +515,10 @@ class SyncReplicasOptimizer(object):
                 self._occupy(engine, comm)
             if end is not None:
                 end.record(comm)
-        return _StreamJoin(comm)
+        join = _StreamJoin(comm)
+        if rccl is not None:
+            self._fc1_join = join
+        return join
 
     # bench.py --occupy: (K, microseconds) — after the fc1 + heads bucket's sum, a launch on the
     # exchange stream holds K CUs for that long (ba3c_occupy_cus), standing in for the CUs

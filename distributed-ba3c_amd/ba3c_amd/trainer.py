@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from .model_desc import ClipByAverageNorm, MapGradient
+from . import hipevent
 from .optimizer import SyncReplicasOptimizer
 
 
@@ -44,7 +45,7 @@ class ExchangeTimeline(object):
         self.steps = []
 
     def new_step(self):
-        ev = {k: torch.cuda.Event(enable_timing=True) for k in self.MAIN + self.COMM}
+        ev = {k: hipevent.timing_event() for k in self.MAIN + self.COMM}
         self.steps.append(ev)
         return ev
 

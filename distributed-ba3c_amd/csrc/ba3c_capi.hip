@@ -1690,9 +1690,14 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id) {
   if (h->ev_begin.empty() && kernel_id >= 0) {
     h->ev_begin.resize(4096);
     h->ev_end.resize(4096);
+    // timestamps only: no system-scope fence (its L2 write-back + invalidate left a 5-6 us
+    // gap around every probed launch, r06a trace)
+    // (BA3C_EVENTS=torch: HIP's default events, the A/B of ba3c_amd/hipevent.py)
+    const char* em = getenv("BA3C_EVENTS");
+    const unsigned fl = (em && std::strcmp(em, "torch") == 0) ? hipEventDefault : hipEventDisableSystemFence;
     for (size_t i = 0; i < h->ev_begin.size(); ++i) {
-      HIP_TRY(hipEventCreate(&h->ev_begin[i]));
-      HIP_TRY(hipEventCreate(&h->ev_end[i]));
+      HIP_TRY(hipEventCreateWithFlags(&h->ev_begin[i], fl));
+      HIP_TRY(hipEventCreateWithFlags(&h->ev_end[i], fl));
     }
   }
   h->probe_kernel = kernel_id;
