@@ -75,6 +75,9 @@ def load():
         "ba3c_train_grads_phase": (i32, [P, P, P, P, P, P, i32, f32, P, P, P, i32]),
         "ba3c_bucket_tensor": (i32, [P]),
         "ba3c_flush_pending": (i32, [P]),
+        "ba3c_launch_held": (i32, [P, P]),
+        "ba3c_set_phase2_event": (i32, [P, P]),
+        "ba3c_clip_grads_range2": (i32, [P, P, P, P, i32, i32, i32]),
         "ba3c_occupy_cus": (i32, [P, i32, ctypes.c_double]),
         "ba3c_apply_update": (i32, [P, P, i32, P, P, P, P, ctypes.POINTER(Ba3cOptParams), f32,
                                     i32, P]),

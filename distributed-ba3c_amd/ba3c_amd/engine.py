@@ -177,11 +177,24 @@ class Ba3cEngine(object):
         t = int(self.lib.ba3c_bucket_tensor(self.h))
         return t, self.layout[t][1]
 
-    def clip_grads_range(self, t0, t1, grads=None):
-        """clip_by_average_norm over tensors [t0, t1) only."""
+    def clip_grads_range(self, t0, t1, grads=None, no_residency=False):
+        """clip_by_average_norm over tensors [t0, t1) only.  no_residency: the two-launch form
+        (for a stream that runs beside other kernels, ba3c_clip_grads_range2)."""
         grads = self.grads if grads is None else grads
-        _lib.check(self.lib.ba3c_clip_grads_range(self.h, _stream(), _ptr(grads),
-                                                  _ptr(self._workspace(True)), int(t0), int(t1)))
+        _lib.check(self.lib.ba3c_clip_grads_range2(self.h, _stream(), _ptr(grads),
+                                                   _ptr(self._workspace(True)), int(t0), int(t1),
+                                                   1 if no_residency else 0))
+
+    def launch_held(self, stream=None):
+        """Launch the fc1 + heads reduction a phase-4 pass held back, on `stream` (a torch
+        stream, default the current one), ordered after the pass's stream."""
+        st = ctypes.c_void_p((stream or torch.cuda.current_stream()).cuda_stream)
+        _lib.check(self.lib.ba3c_launch_held(self.h, st))
+
+    def set_phase2_event(self, event):
+        """Record `event` (a hipevent.HipEvent, or None) after conv3's gradient launches of every
+        later phase-2 pass."""
+        _lib.check(self.lib.ba3c_set_phase2_event(self.h, event._ev if event is not None else None))
 
     def clip_grads(self, grads=None):
         """tf.clip_by_average_norm(g, 0.1) per tensor, in place (train.py:329-330)."""

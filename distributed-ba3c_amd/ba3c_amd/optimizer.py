@@ -455,6 +455,61 @@ class SyncReplicasOptimizer(object):
     _ready_event = None
     _fc1_join = None
 
+    def aggregate_held_bucket_async(self, engine, mid, t0, t1, off0, off1, marks=None):
+        """The N>1 step's first bucket (fc1 + heads) after a phase-4 pass: on the exchange
+        stream, once `mid` (recorded in phase 2 right after conv3's launches) has passed, the
+        held reduction of the bucket's weight gradients, the bucket's clip in its two-launch
+        form (it runs beside phase 2's kernels, so its workgroups cannot assume co-residency)
+        and its sum.  Starting there puts the collective's workgroups at the boundary before
+        conv2's launch, whose short non-persistent workgroups the dispatcher rebalances, rather
+        than beside conv3's persistent ones, and keeps the reduction and the clip off the
+        learner stream.  `marks`: (start, ready, begin, end) timing events on the exchange
+        stream.  Returns the work handle (always: the update must join the exchange stream)."""
+        start, ready, begin, end = marks if marks is not None else (None, None, None, None)
+        dev = engine.grads.device
+        buf = engine.grads[off0:off1]
+        if not buf.is_cuda:                   # CPU engines (tests): no streams
+            engine.launch_held()
+            engine.clip_grads_range(t0, t1)
+            return self._all_reduce(buf, async_op=True) if self.distributed else None
+        rccl = self.direct_rccl(dev) if self.distributed else None   # (collective on first use)
+        comm = self.comm_stream(dev)
+        if isinstance(mid, hipevent.HipEvent):
+            mid.wait(comm)
+        else:
+            comm.wait_event(mid)
+        join = _StreamJoin(comm)
+        with torch.cuda.stream(comm):
+            if start is not None:
+                start.record(comm)
+            engine.launch_held(comm)
+            engine.clip_grads_range(t0, t1, no_residency=True)
+            if ready is not None:
+                ready.record(comm)
+            if not self.distributed:
+                return join
+            if begin is not None:
+                begin.record(comm)
+            if self._staged(buf):
+                host = buf.cpu()              # host-staged (gloo): waits for the clip
+                work = dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                return _StagedWork(work, host, buf, stream=comm, end=end)
+            if rccl is not None:
+                rccl.all_reduce_sum(buf, comm)
+                self._occupy(engine, comm)
+                if self._ar_event is None:
+                    self._ar_event = hipevent.join_event()
+                self._ar_event.record(comm)
+                self._ar_done = self._ar_event
+                self._fc1_join = join
+            else:
+                work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                work.wait()                   # `comm` waits for the collective's stream
+                self._occupy(engine, comm)
+            if end is not None:
+                end.record(comm)
+        return join
+
     def aggregate_bucket_async(self, engine, t0, t1, off0, off1, marks=None, last=False):
         """Clip tensors [t0, t1) and start the RCCL sum of flat range [off0, off1); returns
         the work handle (None when there is nothing to join).  The sum runs on the exchange

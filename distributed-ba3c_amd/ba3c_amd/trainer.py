@@ -33,13 +33,14 @@ class TrainConfig(object):
 
 class ExchangeTimeline(object):
     """HIP timing events of the bucketed data-parallel step (Ba3cTrainer._bucketed_sync_step),
-    recorded inside the real step: on the learner stream `start`, `fc1_ready` (phase 1 + the
-    fc1/heads bucket's clip done), `conv_ready` (phase 2 + the conv bucket's clip done),
-    `exchanged` (both sums joined) and `end` (update applied); on the exchange stream each
-    bucket's all-reduce begin / end.  summary() averages the intervals over the steps."""
+    recorded inside the real step: on the learner stream `start`, `phase1_end`, `conv_ready`
+    (phase 2 + the conv bucket's clip done), `exchanged` (both sums joined) and `end` (update
+    applied); on the exchange stream `fc1_start` (the phase-2 event passed), `fc1_ready` (the
+    held fc1 + heads reduction and the bucket's clip done) and each bucket's all-reduce
+    begin / end.  summary() averages the intervals over the steps."""
 
-    MAIN = ("start", "fc1_ready", "conv_ready", "exchanged", "end")
-    COMM = ("fc1_ar_begin", "fc1_ar_end", "conv_ar_begin", "conv_ar_end")
+    MAIN = ("start", "phase1_end", "conv_ready", "exchanged", "end")
+    COMM = ("fc1_start", "fc1_ready", "fc1_ar_begin", "fc1_ar_end", "conv_ar_begin", "conv_ar_end")
 
     def __init__(self):
         self.steps = []
@@ -53,7 +54,11 @@ class ExchangeTimeline(object):
         """Mean milliseconds of each interval (call after the device has synchronised)."""
         if not self.steps:
             return None
-        keys = {"phase1_ms": ("start", "fc1_ready"), "phase2_ms": ("fc1_ready", "conv_ready"),
+        keys = {"phase1_ms": ("start", "phase1_end"), "phase2_ms": ("phase1_end", "conv_ready"),
+                # exchange stream: the held fc1 + heads reduction and the bucket's clip, from
+                # the phase-2 event (after conv3) on
+                "fc1_prep_ms": ("fc1_start", "fc1_ready"),
+                "fc1_start_after_phase1_ms": ("phase1_end", "fc1_start"),
                 "fc1_allreduce_ms": ("fc1_ar_begin", "fc1_ar_end"),
                 "conv_allreduce_ms": ("conv_ar_begin", "conv_ar_end"),
                 "exposed_ms": ("conv_ready", "exchanged"), "update_ms": ("exchanged", "end"),
@@ -167,18 +172,25 @@ class Ba3cTrainer(object):
         inputs = [state, action, futurereward]
         tl = self.timeline.new_step() if self.timeline is not None else None
         mark = (lambda k: tl[k].record()) if tl is not None else (lambda k: None)
+        if self._mid is None and eng.grads.is_cuda:
+            # recorded by every phase-2 pass after conv3's launches (ba3c_set_phase2_event)
+            self._mid = hipevent.HipEvent(hipevent.HIP_EVENT_DISABLE_TIMING
+                                          | hipevent.HIP_EVENT_RELEASE_TO_DEVICE)
+            eng.set_phase2_event(self._mid)
         mark("start")
-        m.train_phase = 1
         try:
+            m.train_phase = 4          # phase 1, its fc1 + heads reduction held back
             m.build_graph(inputs)
-            # fc1_ready / conv_ready: after the bucket's clip (its sum may start from there)
-            work = opt.aggregate_bucket_async(
-                eng, tb, nt, off, total,
-                marks=tl and (tl["fc1_ready"], tl["fc1_ar_begin"], tl["fc1_ar_end"]))
+            mark("phase1_end")
             m.train_phase = 2
             m.build_graph(inputs)
         finally:
             m.train_phase = 0
+        # the fc1 + heads bucket: held reduction, clip and sum on the exchange stream from the
+        # phase-2 event on, beside conv2..conv0's backward
+        work = opt.aggregate_held_bucket_async(
+            eng, self._mid, tb, nt, off, total,
+            marks=tl and (tl["fc1_start"], tl["fc1_ready"], tl["fc1_ar_begin"], tl["fc1_ar_end"]))
         work2 = opt.aggregate_bucket_async(
             eng, 0, tb, 0, off, last=True,
             marks=tl and (tl["conv_ready"], tl["conv_ar_begin"], tl["conv_ar_end"]))
@@ -190,6 +202,7 @@ class Ba3cTrainer(object):
         mark("end")
 
     timeline = None
+    _mid = None
 
     def capture_step(self, state, action, futurereward, warmup=2):
         """Capture one full step (fwd+bwd+clip+update) on static input tensors as a hipGraph

@@ -160,6 +160,15 @@ struct ba3c_handle {
   const float* pend_grads = nullptr;
   hipEvent_t ev_pend = nullptr;   // orders a flush on the pass's stream before another stream
   bool defer_final = false;   // set by train_grads_impl for phase 3
+  // phase 4 (phase 1 with its reduction held): the fc1 + heads weight-gradient reduction is
+  // kept here, unlaunched, until ba3c_launch_held puts it on the caller's stream (the exchange
+  // stream of the N>1 step); phase 2 does not launch it, every other entry point does
+  bool held = false;
+  hipStream_t held_stream = nullptr;
+  ReduceJobs held_jobs{};
+  // recorded on the pass's stream after conv3's gradient launches of every phase-2 pass
+  // (ba3c_set_phase2_event; null: none)
+  hipEvent_t ev_mid = nullptr;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[4] = {}, ev_join = nullptr;
   // weight-gradient reductions of the running backward pass, launched together at its end
@@ -828,7 +837,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   } defer_guard(h);
   // join the side stream and run the deferred reductions of this phase in one launch
   auto finish = [&]() -> int {
-    if (h->pend_scalars && phase != 1) {   // no launch took the deferred scalar reduction
+    if (h->pend_scalars && phase != 1 && phase != 4) {   // no launch took the deferred scalar reduction
       // (phase 1 leaves it pending: conv3's input-gradient launch in phase 2 takes it)
       const ScalarsJob::Args& sa = h->scalars_args;
       ProbeScope ps(h, s, BA3C_K_SCALARS);
@@ -841,7 +850,11 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
       HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
     }
     const ReduceJobs& jb = h->rjobs;
-    if (jb.n > 0 && h->defer_final && phase == 0) {
+    if (jb.n > 0 && phase == 4) {
+      h->held = true;          // ba3c_launch_held (or the next entry point) launches it
+      h->held_stream = s;
+      h->held_jobs = jb;
+    } else if (jb.n > 0 && h->defer_final && phase == 0) {
       h->pend_reduce = true;   // the next fused apply runs it (flush_reduce otherwise)
       h->pend_stream = s;
       h->pend_grads = grads;
@@ -909,7 +922,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     CHECK(fork());
   }
   }  // phase != 2
-  if (phase == 1) return finish();
+  if (phase == 1 || phase == 4) return finish();
   auto conv_reduce = [&](const WgradPlan& pl, int layer, int cin, int cinpad, const float* part) {
     ReduceMap mp{};
     mp.kind = 0;
@@ -968,6 +981,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     CHECK(conv_reduce(pl, 3, 64, 64, w.part_3));
     CHECK(fork());
   }
+  if (phase == 2 && h->ev_mid) HIP_TRY(hipEventRecord(h->ev_mid, s));
   // conv2
   if (mj) {
     const Wg6Args wa{w.p1, w.dp2, w.c2, w.part_2, B, w.am(AM_P1, h), w.am(AM_DP2, h)};
@@ -1400,6 +1414,7 @@ size_t ba3c_workspace_size(const ba3c_handle* h, int32_t batch, int32_t train) {
 }
 
 static int flush_reduce(ba3c_handle* h, hipStream_t s);
+static int flush_held(ba3c_handle* h, hipStream_t s, bool order = true);
 
 int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                  int32_t batch, float explore_factor, void* workspace, float* probs,
@@ -1409,6 +1424,7 @@ int ba3c_forward(ba3c_handle* h, void* stream, const float* params, const uint8_
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
   CHECK(flush_reduce(h, s));
+  CHECK(flush_held(h, s));
   Workspace w = carve(h, workspace, batch, false);
   std::memset(h->merged, 0, sizeof(h->merged));
   int r = h->cfg.channels == 4 ? run_forward<4>(h, s, params, state, batch, w, false)
@@ -1442,6 +1458,38 @@ static int flush_reduce(ba3c_handle* h, hipStream_t s) {
   return BA3C_OK;
 }
 
+// launch the fc1 + heads reduction a phase-4 pass held back, on stream `s`; `order`: after
+// everything enqueued on the pass's stream so far (an event, when the streams differ).
+// ba3c_launch_held leaves the ordering to its caller (the N>1 step orders the exchange stream
+// after the phase-2 event, i.e. after phase 1, not after the whole of phase 2)
+static int flush_held(ba3c_handle* h, hipStream_t s, bool order) {
+  if (!h || !h->held) return BA3C_OK;
+  h->held = false;
+  if (order && s != h->held_stream) {
+    if (!h->ev_pend) HIP_TRY(hipEventCreateWithFlags(&h->ev_pend, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(h->ev_pend, h->held_stream));
+    HIP_TRY(hipStreamWaitEvent(s, h->ev_pend, 0));
+  }
+  const ReduceJobs& jb = h->held_jobs;
+  {
+    ProbeScope ps(h, s, BA3C_K_WGRAD_REDUCE);
+    hipLaunchKernelGGL(wgrad_reduce_all_kernel, dim3(jb.blk0[jb.n]), dim3(64 * RED_G), 0, s, jb);
+  }
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_launch_held(ba3c_handle* h, void* stream) {
+  if (!h) return fail(BA3C_ERR_INVALID, "null handle");
+  return flush_held(h, static_cast<hipStream_t>(stream), false);
+}
+
+int ba3c_set_phase2_event(ba3c_handle* h, void* event) {
+  if (!h) return fail(BA3C_ERR_INVALID, "null handle");
+  h->ev_mid = static_cast<hipEvent_t>(event);
+  return BA3C_OK;
+}
+
 int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                      const int64_t* action, const float* futurereward, int32_t batch,
                      float entropy_beta, void* workspace, float* grads, double* scalars) {
@@ -1453,7 +1501,7 @@ int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, co
                            const int64_t* action, const float* futurereward, int32_t batch,
                            float entropy_beta, void* workspace, float* grads, double* scalars,
                            int32_t phase) {
-  if (phase < 0 || phase > 3) return fail(BA3C_ERR_INVALID, "phase must be 0, 1, 2 or 3");
+  if (phase < 0 || phase > 4) return fail(BA3C_ERR_INVALID, "phase must be 0, 1, 2, 3 or 4");
   if (phase != 3)
     return train_grads_impl(h, stream, params, state, action, futurereward, batch, entropy_beta, workspace,
                             grads, scalars, phase);
@@ -1468,7 +1516,8 @@ int ba3c_bucket_tensor(const ba3c_handle* h) { return h ? h->idx_fc1 : -1; }
 
 int ba3c_flush_pending(ba3c_handle* h) {
   if (!h) return fail(BA3C_ERR_INVALID, "null handle");
-  return flush_reduce(h, h->pend_stream);
+  CHECK(flush_reduce(h, h->pend_stream));
+  return flush_held(h, h->held_stream);
 }
 
 static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
@@ -1481,6 +1530,7 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
   if (batch < 1 || batch > h->cfg.max_batch) return fail(BA3C_ERR_INVALID, "batch out of range");
   hipStream_t s = static_cast<hipStream_t>(stream);
   CHECK(flush_reduce(h, s));
+  if (phase != 2) CHECK(flush_held(h, s));   // phase 2 runs beside the held reduction
   CHECK(ensure_side_stream(h, s));
   Workspace w = carve(h, workspace, batch, true);
   // no memset of `grads`: the backward pass's single reduction launch writes every element
@@ -1505,14 +1555,21 @@ static int train_grads_impl(ba3c_handle* h, void* stream, const float* params, c
 
 int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* workspace, int32_t t0,
                           int32_t t1) {
+  return ba3c_clip_grads_range2(h, stream, grads, workspace, t0, t1, 0);
+}
+
+int ba3c_clip_grads_range2(ba3c_handle* h, void* stream, float* grads, void* workspace, int32_t t0,
+                           int32_t t1, int32_t flags) {
   if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
   if (t0 < 0 || t1 > h->table.n || t0 >= t1) return fail(BA3C_ERR_INVALID, "bad tensor range");
+  if (flags & ~BA3C_CLIP_NO_RESIDENCY) return fail(BA3C_ERR_INVALID, "unknown clip flags");
   hipStream_t s = static_cast<hipStream_t>(stream);
   CHECK(flush_reduce(h, s));
+  if (t1 > h->idx_fc1) CHECK(flush_held(h, s));   // the range holds tensors the held reduction writes
   float* part = carve(h, workspace, 1, false).sumsq;
   const int c0 = h->table.chunk0[t0], nc = h->table.chunk0[t1] - c0;
   ProbeScope ps(h, s, BA3C_K_CLIP);
-  if (h->ctag && h->fused_update && nc <= h->cus) {
+  if (h->ctag && h->fused_update && nc <= h->cus && !(flags & BA3C_CLIP_NO_RESIDENCY)) {
     // one launch (tagged partials), bit-identical to the two below
     const UpdateSync us{h->ctag, reinterpret_cast<unsigned int*>(h->ctag + h->table.nchunks)};
     hipLaunchKernelGGL(clip_range_kernel, dim3(nc), dim3(256), 0, s, grads, h->table, c0, us);
@@ -1528,6 +1585,7 @@ int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace)
   if (!h || !check_ptr(grads) || !check_ptr(workspace)) return fail(BA3C_ERR_INVALID, "null pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
   CHECK(flush_reduce(h, s));
+  CHECK(flush_held(h, s));
   float* part = carve(h, workspace, 1, false).sumsq;  // batch-independent first region
   {
     ProbeScope ps(h, s, BA3C_K_CLIP);
@@ -1598,6 +1656,7 @@ static int apply_update_impl(ba3c_handle* h, void* stream, int32_t opt, float* p
 #undef BA3C_RCU
   }
   CHECK(flush_reduce(h, s));
+  CHECK(flush_held(h, s));
   if (fused) {
     a.clip_part = part;
     const dim3 grid(h->table.nchunks);
@@ -1807,6 +1866,7 @@ int ba3c_device_errors(ba3c_handle* h, uint32_t* flags) {
   if (!h || !flags) return fail(BA3C_ERR_INVALID, "null argument");
   *flags = 0;
   CHECK(flush_reduce(h, h->pend_stream));
+  CHECK(flush_held(h, h->held_stream));
   if (!h->utag) return BA3C_OK;
   // every stream, the non-blocking ones torch creates included (a null-stream copy does not
   // wait for those)

@@ -156,13 +156,30 @@ int ba3c_train_grads(ba3c_handle* h, void* stream, const float* params, const ui
  * clip + update as ONE chained launch (a launch fewer per step, but measured 4 us slower at
  * configs[1]: the trainer uses it only with BA3C_DEFER_REDUCE=1); any other entry
  * point on the handle (forward, train, clip, an unfused or mismatched apply, device_errors)
- * first launches it on the pass's stream (a call on another stream then waits for it).  `grads` holds the raw gradients only after that. */
+ * first launches it on the pass's stream (a call on another stream then waits for it).  `grads` holds the raw gradients only after that.
+ * Phase 4 = phase 1 with the fc1 + heads reduction HELD: nothing launches it until
+ * ba3c_launch_held(h, stream) puts it on the caller's stream (after the pass's stream), so the
+ * N>1 step can run it, the bucket clip and the bucket's all-reduce on its exchange stream
+ * while phase 2 runs; phase 2 does not launch it, every other entry point does (on its own
+ * stream, after the pass's). */
 int ba3c_train_grads_phase(ba3c_handle* h, void* stream, const float* params, const uint8_t* state,
                            const int64_t* action, const float* futurereward, int32_t batch,
                            float entropy_beta, void* workspace, float* grads, double* scalars,
                            int32_t phase);
+/* Launch the reduction a phase-4 pass held back, on `stream`; no-op when none is held.  The
+ * caller orders `stream` after the phase-4 pass (e.g. by waiting for the ba3c_set_phase2_event
+ * event, which follows it); the implicit launches of the other entry points order themselves
+ * after everything enqueued on the pass's stream.  Replaces the PS push of the fc1 + heads
+ * variables' gradients of OpenAIGym/train.py:598-606 (their aggregation starts from here). */
+int ba3c_launch_held(ba3c_handle* h, void* stream);
+/* Record the HIP event `event` (a hipEvent_t of the caller's, NULL: none) on the pass's stream
+ * in every later phase-2 pass, right after conv3's gradient launches: the N>1 step starts the
+ * fc1 + heads bucket's exchange from there, so its collective's workgroups take CUs at the
+ * boundary before conv2's launch (short, non-persistent workgroups the dispatcher rebalances)
+ * instead of beside conv3's persistent ones. */
+int ba3c_set_phase2_event(ba3c_handle* h, void* event);
 /* Launch a reduction that a phase-3 pass left pending, on the pass's stream (no-op when none
- * is pending).  For callers that read `grads` through another API (a torch view, a gradient
+ * is pending; also launches a held phase-4 reduction).  For callers that read `grads` through another API (a torch view, a gradient
  * summary) between the pass and the fused apply. */
 int ba3c_flush_pending(ba3c_handle* h);
 /* First tensor of the fc1 + heads bucket (tensors before it: the conv layers). */
@@ -171,6 +188,12 @@ int ba3c_bucket_tensor(const ba3c_handle* h);
 /* Per-tensor tf.clip_by_average_norm(g, 0.1) in place (n = graph numel incl. padding). */
 int ba3c_clip_grads(ba3c_handle* h, void* stream, float* grads, void* workspace);
 /* The same clip over tensors [t0, t1) only (a bucket). */
+/* ba3c_clip_grads_range with flags: BA3C_CLIP_NO_RESIDENCY makes no co-residency
+ * assumption (sum-of-squares + clip launches instead of the one-launch tagged form, whose
+ * workgroups wait for each other): for a clip on a stream that runs beside other kernels. */
+#define BA3C_CLIP_NO_RESIDENCY 1
+int ba3c_clip_grads_range2(ba3c_handle* h, void* stream, float* grads, void* workspace, int32_t t0,
+                           int32_t t1, int32_t flags);
 int ba3c_clip_grads_range(ba3c_handle* h, void* stream, float* grads, void* workspace, int32_t t0,
                           int32_t t1);
 

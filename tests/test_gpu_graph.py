@@ -245,6 +245,64 @@ def test_two_phase_backward_equals_one_pass(B):
     assert torch.equal(sc1, sc)
 
 
+@pytest.mark.parametrize("B", [32, 2048])
+def test_held_phase1_reduction_on_exchange_stream_equals_one_pass(B):
+    """The N>1 step's order (trainer.py _bucketed_sync_step): phase 4 (phase 1 with the fc1 +
+    heads reduction held), phase 2 recording the handle's phase-2 event after conv3, then on a
+    second stream that waits for the event the held reduction (ba3c_launch_held) and the
+    bucket's clip in its two-launch form (ba3c_clip_grads_range2 BA3C_CLIP_NO_RESIDENCY).
+    Gradients equal the one-pass gradients bit for bit (B=2048: the bench's persistent
+    kernels), the clipped bucket equals the one-launch clip of the same gradients, phase 2
+    leaves the bucket alone, and no in-launch wait gave up."""
+    from ba3c_amd import hipevent
+    from ba3c_amd.engine import Ba3cEngine
+    F, S = (128, 4) if B == 32 else (512, 1)
+    rs = np.random.RandomState(83)
+    state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    eng = Ba3cEngine(num_actions=4, fc_neurons=F, fc_splits=S, max_batch=B)
+    eng.load_params(O.init_params(F, S, 4, seed=13, dtype=np.float32))
+    tb, off = eng.bucket_split()
+    nt = len(eng.layout)
+    sc = eng.train_grads(state, action, R).clone()
+    ref = eng.grads.clone()
+    eng.clip_grads_range(tb, nt)                 # one-launch clip of the bucket
+    ref_clip = eng.grads[off:].clone()
+    mid = hipevent.HipEvent(hipevent.HIP_EVENT_DISABLE_TIMING | hipevent.HIP_EVENT_RELEASE_TO_DEVICE)
+    eng.set_phase2_event(mid)
+    side = torch.cuda.Stream()
+    for _ in range(2):                           # a second step on the same handle
+        eng.grads.fill_(0.5)
+        eng.train_grads(state, action, R, phase=4)
+        sc2 = eng.train_grads(state, action, R, phase=2)
+        mid.wait(side)
+        eng.launch_held(side)
+        hipevent.wait_stream(torch.cuda.current_stream(), side)
+        torch.cuda.synchronize()
+        for i, (name, o, n, _) in enumerate(eng.layout):
+            assert torch.equal(eng.grads[o:o + n], ref[o:o + n]), name
+        assert torch.equal(sc2, sc)
+        with torch.cuda.stream(side):
+            eng.clip_grads_range(tb, nt, no_residency=True)
+        torch.cuda.synchronize()
+        _bucket_equal(eng, tb, off, ref_clip)
+    eng.set_phase2_event(None)
+    # an unlaunched held reduction is launched by the next entry point on its own stream
+    eng.train_grads(state, action, R, phase=4)
+    eng.train_grads(state, action, R, phase=2)
+    eng.clip_grads_range(tb, nt, no_residency=True)
+    torch.cuda.synchronize()
+    _bucket_equal(eng, tb, off, ref_clip)
+    assert eng.device_errors() == 0
+
+
+def _bucket_equal(eng, tb, off, ref_clip):
+    for i, (name, o, n, _) in enumerate(eng.layout):     # tensors only (not the alignment gaps)
+        if i >= tb:
+            assert torch.equal(eng.grads[o:o + n], ref_clip[o - off:o - off + n]), name
+
+
 def test_one_launch_bucket_clip_matches_two_launch_clip(monkeypatch):
     """ba3c_clip_grads_range (the data-parallel step's per-bucket clip, train.py:329-330 per
     replica) runs as ONE launch with tagged partials (clip_range_kernel); BA3C_FUSED_UPDATE=0

@@ -65,16 +65,22 @@ class OracleEngine(object):
             self.scalars[0] = float(sc["cost"])
         if phase == 0:
             self.grads.copy_(self._full)
-        elif phase == 1:
+        elif phase in (1, 4):               # 4: phase 1 whose reduction the HIP engine holds
             self.grads[off:].copy_(self._full[off:])
         else:
             self.grads[:off].copy_(self._full[:off])
         return self.scalars
 
+    def launch_held(self, stream=None):
+        pass                                 # the held reduction: nothing to launch on the CPU
+
+    def set_phase2_event(self, event):
+        pass
+
     def clip_grads(self, grads=None):
         self.clip_grads_range(0, len(self.names))
 
-    def clip_grads_range(self, t0, t1, grads=None):
+    def clip_grads_range(self, t0, t1, grads=None, no_residency=False):
         g = self.state_dict(self.grads)
         for k in self.names[t0:t1]:
             n = int(np.prod(self.shapes[k]))
