@@ -225,28 +225,41 @@ def sync_all(world):
 
 
 def time_steps(tr, batch, steps, warmup, world, probe=None):
-    """Time exactly `steps` steps bracketed by barrier + synchronize (max over ranks), and
-    each step's own HIP-event interval on the learner stream (for the median)."""
+    """Time exactly `steps` steps bracketed by barrier + synchronize (max over ranks): the
+    wall clock, and HIP events around the whole run on the learner stream.  Then, outside the
+    timed region, `steps` more steps with an event after each (every event recorded on the
+    learner stream leaves a 5-6 us gap between its kernels, r06c trace) for the per-step
+    median."""
     for _ in range(warmup):
         tr.train_step(*batch)
     sync_all(world)
     if probe is not None:
         tr.engine.probe_enable(probe)   # bracket the dominant kernel over the timed steps only
-    evs = [hipevent.timing_event() for _ in range(steps + 1)]   # no system fence (hipevent.py)
+    e0, e1 = hipevent.timing_event(), hipevent.timing_event()   # no system fence (hipevent.py)
     t0 = time.perf_counter()
+    e0.record()
+    for i in range(steps):
+        tr.train_step(*batch)
+    e1.record()
+    sync_all(world)
+    wall = time.perf_counter() - t0
+    gpu_s = e0.elapsed_time(e1) / 1000.0
+    probe_ms, launches = 0.0, 0
+    if probe is not None:
+        probe_ms, launches = tr.engine.probe_read()   # the probe covers the timed steps only
+        tr.engine.probe_enable(None)
+    evs = [hipevent.timing_event() for _ in range(steps + 1)]
     evs[0].record()
     for i in range(steps):
         tr.train_step(*batch)
         evs[i + 1].record()
     sync_all(world)
-    wall = time.perf_counter() - t0
     per_step = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
-    gpu_s = sum(per_step) / 1000.0
     el = torch.tensor([max(wall, gpu_s), float(np.median(per_step))], dtype=torch.float64,
                       device="cuda")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    return float(el[0].item()), float(el[1].item())
+    return float(el[0].item()), float(el[1].item()), probe_ms, launches
 
 
 def time_graph_steps(tr, batch, steps, warmup):
@@ -358,15 +371,25 @@ def occupy_table(tr, batch, ks, window_us, phase2_us, iters, world, probe, base)
     return rows
 
 
-def exchange_report(tr, batch, timeline, iters, world, occupy=(), occupy_us=50.0):
-    """N > 1 (or --sync-path): where the data-parallel exchange's time goes.  `timeline` holds
-    the HIP events the timed steps recorded inside the real bucketed step (ExchangeTimeline:
-    phase 1, phase 2, each bucket's all-reduce from its clip to its end on the exchange
-    stream, the exposed wait, the update); every field is the max over ranks.  After the
-    timed region each phase-2 launch is probed over `iters` steps with the exchange running
+def exchange_report(tr, batch, iters, world, occupy=(), occupy_us=50.0):
+    """N > 1 (or --sync-path): where the data-parallel exchange's time goes.  After the timed
+    region, `iters` real bucketed steps record HIP events inside the step (ExchangeTimeline:
+    phase 1, phase 2, the exchange stream's start after the phase-2 event, each bucket's
+    all-reduce, the exposed wait, the update); every field is the max over ranks.  The marks
+    are kept out of the timed steps: each event recorded on the learner stream costs a
+    5-6 us gap between its kernels (r06c trace), so `timeline.step_ms` includes about seven of
+    them.  Then each phase-2 launch is probed over `iters` steps with the exchange running
     and with it left out (each rank applies its own gradients; replicas diverge from here),
     so the cost of RCCL sharing CUs with the persistent conv kernels shows per launch."""
+    from ba3c_amd.trainer import ExchangeTimeline
     opt, eng = tr.optimizer, tr.engine
+    timeline = ExchangeTimeline()
+    tr.timeline = timeline
+    sync_all(world)
+    for _ in range(iters):
+        tr.train_step(*batch)
+    sync_all(world)
+    tr.timeline = None
     tb, off = eng.bucket_split()
     rccl_comms = None
     if dist.is_initialized():
@@ -606,7 +629,6 @@ def main():
 
 
 def run_rank(args, world, rank, local):
-    from ba3c_amd.trainer import ExchangeTimeline
     if args.dist_backend == "gloo":
         # rehearsal of N ranks on fewer GPUs: the exchange goes through a host copy
         local = local % torch.cuda.device_count()
@@ -633,21 +655,13 @@ def run_rank(args, world, rank, local):
     dom = os.environ.get("BA3C_BENCH_PROBE", dom)
     sync_all(world)
 
-    timeline = None
-    if sync:
-        timeline = ExchangeTimeline()
-        tr.timeline = timeline          # events inside the real bucketed step
-    elapsed, med_ms = time_steps(tr, batch, args.steps, args.warmup, world, probe=dom)
-    probe_ms, launches = tr.engine.probe_read()
-    tr.engine.probe_enable(None)
+    elapsed, med_ms, probe_ms, launches = time_steps(tr, batch, args.steps, args.warmup, world,
+                                                     probe=dom)
     flags = tr.engine.device_errors()     # synchronises; after the timed region
     identical = None
     if world > 1:
         inner = tr.optimizer._opt if hasattr(tr.optimizer, "_opt") else tr.optimizer
         identical = replicas_identical([tr.engine.params] + list(inner.slots or []))
-    if timeline is not None:
-        # keep only the timed steps' events
-        timeline.steps = timeline.steps[-args.steps:]
 
     value = world * B * args.steps / elapsed
     ms_step = elapsed / args.steps * 1000.0
@@ -709,8 +723,8 @@ def run_rank(args, world, rank, local):
     rc = health(out, flags, identical)
     if sync:
         ks = [int(k) for k in args.occupy.split(",") if k.strip()]
-        out["exchange"] = exchange_report(tr, batch, timeline, max(args.steps // 3, 5), world,
-                                          ks, args.occupy_us)
+        out["exchange"] = exchange_report(tr, batch, max(args.steps // 3, 5), world, ks,
+                                          args.occupy_us)
     if not args.no_overlap:
         out["overlap"] = overlap_bench(tr, batch, args.predict_batch, 10, world)
     if not args.no_b32:
@@ -719,7 +733,7 @@ def run_rank(args, world, rank, local):
         tr = None
         tr32, b32 = build_trainer(32, 128, 4, A, world, seed=rank, sync=sync)
         n32 = max(args.steps, 100)
-        el32, med32 = time_steps(tr32, b32, n32, 10, world)
+        el32, med32, _, _ = time_steps(tr32, b32, n32, 10, world)
         out["b32"] = {"config": "configs[1]: B=32/GPU, fc_neurons=128, fc_splits=4",
                       "value": round(world * 32 * n32 / el32, 1), "unit": "samples/s",
                       "ms_per_step": round(el32 / n32 * 1000.0, 4),

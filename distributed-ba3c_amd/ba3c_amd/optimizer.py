@@ -455,22 +455,24 @@ class SyncReplicasOptimizer(object):
     _ready_event = None
     _fc1_join = None
 
-    def aggregate_held_bucket_async(self, engine, mid, t0, t1, off0, off1, marks=None):
-        """The N>1 step's first bucket (fc1 + heads) after a phase-4 pass: on the exchange
-        stream, once `mid` (recorded in phase 2 right after conv3's launches) has passed, the
-        held reduction of the bucket's weight gradients, the bucket's clip in its two-launch
-        form (it runs beside phase 2's kernels, so its workgroups cannot assume co-residency)
-        and its sum.  Starting there puts the collective's workgroups at the boundary before
-        conv2's launch, whose short non-persistent workgroups the dispatcher rebalances, rather
-        than beside conv3's persistent ones, and keeps the reduction and the clip off the
-        learner stream.  `marks`: (start, ready, begin, end) timing events on the exchange
-        stream.  Returns the work handle (always: the update must join the exchange stream)."""
+    def aggregate_held_bucket_async(self, engine, mid, t0, t1, off0, off1, marks=None, held=True):
+        """The N>1 step's first bucket (fc1 + heads): on the exchange stream, once `mid`
+        (recorded in phase 2 right after conv3's launches) has passed, the bucket's sum.
+        Starting there puts the collective's workgroups at the boundary before conv2's launch,
+        whose short non-persistent workgroups the dispatcher rebalances, rather than beside
+        conv3's persistent ones.  `held` (a phase-4 pass, BA3C_XCHG_HELD=1): the held reduction
+        of the bucket's weight gradients and the bucket's clip in its two-launch form (it runs
+        beside phase 2's kernels, so its workgroups cannot assume co-residency) run there
+        first; otherwise the caller clipped the bucket on its own stream after phase 1.
+        `marks`: (start, ready, begin, end) timing events on the exchange stream.  Returns the
+        work handle (always: the update must join the exchange stream)."""
         start, ready, begin, end = marks if marks is not None else (None, None, None, None)
         dev = engine.grads.device
         buf = engine.grads[off0:off1]
         if not buf.is_cuda:                   # CPU engines (tests): no streams
-            engine.launch_held()
-            engine.clip_grads_range(t0, t1)
+            if held:
+                engine.launch_held()
+                engine.clip_grads_range(t0, t1)
             return self._all_reduce(buf, async_op=True) if self.distributed else None
         rccl = self.direct_rccl(dev) if self.distributed else None   # (collective on first use)
         comm = self.comm_stream(dev)
@@ -482,8 +484,9 @@ class SyncReplicasOptimizer(object):
         with torch.cuda.stream(comm):
             if start is not None:
                 start.record(comm)
-            engine.launch_held(comm)
-            engine.clip_grads_range(t0, t1, no_residency=True)
+            if held:
+                engine.launch_held(comm)
+                engine.clip_grads_range(t0, t1, no_residency=True)
             if ready is not None:
                 ready.record(comm)
             if not self.distributed:

@@ -93,6 +93,14 @@ class Ba3cTrainer(object):
         if flag not in ("0", "1"):
             raise ValueError("BA3C_DEFER_REDUCE must be 0 or 1 (got %r)" % flag)
         self._defer_reduce = flag == "1"
+        # BA3C_XCHG_HELD=1: the N>1 step holds phase 1's fc1 + heads reduction and runs it and
+        # the bucket's clip on the exchange stream (ba3c_launch_held).  Default 0: same-box
+        # r06c, the held work beside conv2's launch stretched that launch by 24 us, more than
+        # the ~16 us it took off the learner stream
+        flag = os.environ.get("BA3C_XCHG_HELD", "0")
+        if flag not in ("0", "1"):
+            raise ValueError("BA3C_XCHG_HELD must be 0 or 1 (got %r)" % flag)
+        self._xchg_held = flag == "1"
         if isinstance(self.optimizer, SyncReplicasOptimizer):
             self.optimizer.broadcast_variables(self.engine)
 
@@ -177,19 +185,24 @@ class Ba3cTrainer(object):
             self._mid = hipevent.HipEvent(hipevent.HIP_EVENT_DISABLE_TIMING
                                           | hipevent.HIP_EVENT_RELEASE_TO_DEVICE)
             eng.set_phase2_event(self._mid)
+        held = self._xchg_held
         mark("start")
         try:
-            m.train_phase = 4          # phase 1, its fc1 + heads reduction held back
+            # phase 1; BA3C_XCHG_HELD=1: phase 4, its fc1 + heads reduction held back for the
+            # exchange stream
+            m.train_phase = 4 if held else 1
             m.build_graph(inputs)
             mark("phase1_end")
+            if not held:
+                eng.clip_grads_range(tb, nt)     # the bucket's clip (one launch)
             m.train_phase = 2
             m.build_graph(inputs)
         finally:
             m.train_phase = 0
-        # the fc1 + heads bucket: held reduction, clip and sum on the exchange stream from the
-        # phase-2 event on, beside conv2..conv0's backward
+        # the fc1 + heads bucket's sum on the exchange stream from the phase-2 event on, beside
+        # conv2..conv0's backward (held: its reduction and clip first)
         work = opt.aggregate_held_bucket_async(
-            eng, self._mid, tb, nt, off, total,
+            eng, self._mid, tb, nt, off, total, held=held,
             marks=tl and (tl["fc1_start"], tl["fc1_ready"], tl["fc1_ar_begin"], tl["fc1_ar_end"]))
         work2 = opt.aggregate_bucket_async(
             eng, 0, tb, 0, off, last=True,
