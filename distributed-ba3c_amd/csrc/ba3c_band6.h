@@ -96,7 +96,21 @@ struct Band6Args {
   const uint32_t* amax_in;
   const int* wexp;
   uint32_t* amax_out;
+  // ring walks only (conv_band6r_kernel): non-null = a dynamic image queue (one ticket word,
+  // zeroed by the step's weight-prep launch); null = static contiguous image ranges
+  unsigned* ticket;
 };
+
+// Dynamic image queue of the ring walks (BA3C_DYNQ, default on where a workgroup walks several
+// images): thread 0 draws the next image with one agent-scope atomic when the workgroup STARTS
+// an image and parks it in an LDS slot one band later, so the round trip hides behind the
+// band's work; the workgroup reads it at the image's end.  Every image's outputs depend only on
+// the image, so the results equal the static partition's bit for bit; what changes is that a
+// workgroup held off the chip (a collective's workgroups on its CU) no longer leaves its images
+// for the end of the launch.
+__device__ __forceinline__ unsigned draw_ticket(unsigned* t) {
+  return __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // packed 16-bit halves: 0xFFFF where the half is zero, else 0 (code-mask of the pooled staging)
 __device__ __forceinline__ uint32_t mask16_eq0(uint32_t d) {
@@ -502,15 +516,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
 // the one-band kernel's, so the outputs are bit-identical.  (Round 2 ran the copy and the new-row
 // stores with no barrier in between: a cross-wave write-after-read race in LDS; fixed in r03.)
 template <class L, bool PRE_ = L::G::SRC == 1>
-__device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, char* lds) {
+__device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, char* lds, int* tslot) {
   static_assert(L::NPH == 1 && L::G::SROWS > L::G::RB, "ring walk: unphased layouts with a halo");
+  static_assert(L::G::NBANDS >= 3, "dynamic queue: the ticket is parked at band 1 and read after the last");
   using O = Band6Ops<L>;
   using G = typename L::G;
   constexpr int HALO = G::SROWS - G::RB;                    // KH - 1 rows carried over
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float us2 = L::NS == 2 ? exp2i(-a.wexp[0]) : 1.0f;
+  const bool dyn = a.ticket != nullptr;
   const int ipw = (a.batch + gx - 1) / gx;
-  const int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
+  int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
+  if (dyn) {
+    if (tid == 0) *tslot = (int)draw_ticket(a.ticket);
+    __syncthreads();
+    img0 = *tslot;
+    img1 = a.batch;
+  }
   // PRE (input-gradient layouts, whose registers allow it): the next band's RB new rows are
   // loaded into registers before this band's MFMAs, so their global latency hides behind them
 #ifndef BA3C_RING_PRE
@@ -522,14 +544,17 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
   float4 pv[PRE ? NNEW : 1];
   uint32_t pc[PRE ? NNEW : 1];
   unsigned long long pos = 0;
-  for (int img = img0; img < img1; ++img) {
+  for (int img = img0; img < img1;) {
     const int ka = L::NS == 2 ? amax_exp(a.amax_in[1 + img]) : 0;   // per-image operand scale
     const float asc = exp2i(ka), us1 = exp2i(-ka);
     float omax = 0.f;
+    unsigned nt = 0;
+    if (dyn && tid == 0) nt = draw_ticket(a.ticket);        // the image after this one
     for (int bi = 0; bi < G::NBANDS; ++bi) {
       const int y0 = bi * G::RB;
       const int rows_out = min(G::RB, G::HO - y0);
       __syncthreads();                                      // previous band's LDS reads are done
+      if (dyn && tid == 0 && bi == 1) *tslot = (int)nt;     // (read after the image's last band)
       unsigned fbase = 0;
 #ifndef BA3C_DIAG_NOSTAGE
 #define BA3C_DIAG_NOSTAGE 0   // diagnostics only (A/B timing builds): skip the band staging
@@ -579,6 +604,7 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
       if (!BA3C_DIAG_NOCOMPUTE) O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [](int) {});
     }
     if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
+    img = dyn ? *tslot : img + 1;   // (written at band 1; bands >= 2 put barriers in between)
   }
   if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
@@ -593,22 +619,30 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
 // image is bit for bit the one store1 builds.
 
 template <class L>
-__device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int gx, char* lds) {
+__device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int gx, char* lds, int* tslot) {
   using O = Band6Ops<L>;
   using G = typename L::G;
   using SP = SplitP<L::NS>;
   constexpr int HALO = G::SROWS - G::RB;
   static_assert(L::NS == 2 && G::SRC == 1 && L::NPH == 1 && !G::POOL && G::PADY == HALO &&
                 G::RB % 2 == 0 && G::UHO == 2 * G::UPH && G::UWO == 2 * G::UPW &&
-                G::UWO + 2 * G::PADX == G::WS && G::HO % G::RB == 0,
+                G::UWO + 2 * G::PADX == G::WS && G::HO % G::RB == 0 && G::NBANDS >= 2,
                 "pooled staging: padded input-gradient rings with whole windows per band");
   constexpr int Q = O::Q;                                   // float4 per pixel
   constexpr int NPI = (G::RB / 2) * G::UPW * Q;             // pooled items of the new rows
   constexpr int IT = (NPI + 255) / 256;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float us2 = exp2i(-a.wexp[0]);
+  const bool dyn = a.ticket != nullptr;
   const int ipw = (a.batch + gx - 1) / gx;
-  const int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
+  int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
+  if (dyn) {
+    if (tid == 0) *tslot = (int)draw_ticket(a.ticket);
+    __syncthreads();
+    img0 = *tslot;
+    img1 = a.batch;
+    __syncthreads();                                        // before the slot is written again
+  }
 
   // pooled rows bi * RB / 2 .. of image img (new rows of band bi: un-pooled rows y0 .. y0 +
   // RB - 1 = staged rows HALO ..); rows past the map load as zero (value and code 0: the
@@ -661,13 +695,17 @@ __device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int g
   uint32_t pc[IT];
   if (img0 < img1) load_items(img0, 0, pv, pc);
   unsigned long long pos = 0;
-  for (int img = img0; img < img1; ++img) {
+  for (int img = img0; img < img1;) {
     const int ka = amax_exp(a.amax_in[1 + img]);            // per-image operand scale
     const float asc = exp2i(ka), us1 = exp2i(-ka);
     float omax = 0.f;
+    unsigned nt = 0;
+    if (dyn && tid == 0) nt = draw_ticket(a.ticket);        // the image after this one
+    int nimg = img + 1;
     for (int bi = 0; bi < G::NBANDS; ++bi) {
       const int y0 = bi * G::RB;
       __syncthreads();                                      // previous band's LDS reads are done
+      if (dyn && tid == 0 && bi == 1) *tslot = (int)nt;     // read after the store barrier below
       if (bi > 0) {
         // halo rows RB .. SROWS-1 -> 0 .. HALO-1; every wave's copy completes before any wave
         // stores new rows over the source rows
@@ -682,25 +720,28 @@ __device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int g
       }
       store_items(pv, pc, asc);
       __syncthreads();
+      if (dyn && bi == 1) nimg = *tslot;
       {
         // prefetch the workgroup's next band (the next image's first band after the last)
         const int nb = bi + 1 < G::NBANDS ? bi + 1 : 0;
-        const int ni = bi + 1 < G::NBANDS ? img : img + 1;
+        const int ni = bi + 1 < G::NBANDS ? img : nimg;
         if (ni < img1) load_items(ni, nb, pv, pc);
       }
       O::compute(a, lds, wave, lane, img, y0, G::RB, us1, us2, pos, omax, [](int) {});
     }
     amax_publish(a.amax_out, img, omax, lane);
+    img = nimg;
   }
 }
 
 template <class L, bool PRE_ = L::G::SRC == 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) conv_band6r_kernel(const Band6Args a) {
   __shared__ uint4 lds4[L::LDS_BYTES / 16];
+  __shared__ int tslot[1];
   if constexpr (BA3C_UNPOOL_STAGE && L::G::SRC == 1 && L::NS == 2)
-    band6r_up_body<L>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
+    band6r_up_body<L>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4), tslot);
   else
-    band6r_body<L, PRE_>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4));
+    band6r_body<L, PRE_>(a, blockIdx.x, gridDim.x, reinterpret_cast<char*>(lds4), tslot);
 }
 
 // conv1's 2:4-sparse input gradient (ba3c_dgrad1s.h): geometry and the B operand of its

@@ -152,6 +152,9 @@ struct ba3c_handle {
   // weight-fragment stream and its staging, which two workgroups per CU do not hide, cost
   // 0.07 and 0.13 ms)
   bool c1s = false;
+  // ring walks with several images per workgroup draw their images from a dynamic queue
+  // (Band6Args::ticket); BA3C_DYNQ=0: static contiguous ranges.  Bit-identical either way
+  bool dynq = true;
   // ba3c_train_grads_phase(phase 3): the pass's weight-gradient reduction is left pending and
   // the next fused-clip apply on the handle runs it as the signalling job of a chained launch
   // (reduce -> clip + update, one launch fewer); any other entry point launches it first
@@ -258,6 +261,11 @@ constexpr int WT_C1F = 0, WT_C2F = WT_C1F + 800 * 32, WT_C3F = WT_C2F + 800 * 64
               WT_C0S = WT_C0F + 32 * Conv0Geom::KDIM,            // uint4 [Conv0S::WB_U4]
               WT_TOTAL = WT_C0S + 4 * Conv0S::WB_U4;
 
+// max-|x| slot arrays (ba3c_split.h, fp16 family)
+enum { AM_P0 = 0, AM_P1 = 1, AM_DP0 = 2, AM_DP1 = 3, AM_DP2 = 4, AM_P2 = 5, AM_DY3 = 6, AMAX_N = 7 };
+// dynamic image-queue tickets of the ring walks (Band6Args::ticket), right after the max slots
+// so the step's weight-prep launch zeroes them with those
+enum { TK_C1F = 0, TK_C1D = 1, TK_N = 4 };
 struct Workspace {
   float *p0, *p1, *p2, *a3, *h, *fcpart, *dh, *dy3, *dp2, *dp1, *dp0, *dzv, *terms, *part0, *sumsq, *wt;
   // split-K / per-workgroup partial slabs of each weight gradient (reduced in one launch at the
@@ -270,9 +278,8 @@ struct Workspace {
   int* wexp;       // [8]: weight scale exponents (wprep jobs WJ_*, conv0 = WX_CONV0)
   size_t bytes;
   uint32_t* am(int t, const ba3c_handle* h) const { return amax + (size_t)t * (1 + h->cfg.max_batch); }
+  unsigned* ticket(int k, const ba3c_handle* h) const { return amax + (size_t)AMAX_N * (1 + h->cfg.max_batch) + k; }
 };
-// max-|x| slot arrays (ba3c_split.h, fp16 family)
-enum { AM_P0 = 0, AM_P1 = 1, AM_DP0 = 2, AM_DP1 = 3, AM_DP2 = 4, AM_P2 = 5, AM_DY3 = 6, AMAX_N = 7 };
 // weight-preparation jobs (forward copies first: inference prepares only those) and the
 // index of each one's scale exponent in Workspace::wexp
 enum { WJ_C1F = 0, WJ_C2F = 1, WJ_C3F = 2, WJ_C1D = 3, WJ_C2D = 4, WJ_C3D = 5, WJ_C1S = 6, WJ_N = 7, WJ_FWD = 3,
@@ -350,7 +357,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   // The clip / optimizer per-chunk sum-of-squares partials come FIRST, at a batch-independent
   // offset: ba3c_clip_grads / ba3c_apply_update receive only the workspace base.
   w.sumsq = (float*)take((size_t)h->table.nchunks * 4);
-  w.amax = (uint32_t*)take((size_t)AMAX_N * (1 + h->cfg.max_batch) * 4);
+  w.amax = (uint32_t*)take(((size_t)AMAX_N * (1 + h->cfg.max_batch) + TK_N) * 4);
   w.wexp = (int*)take(8 * 4);
   w.p0 = (float*)take(Bz * P0 * 4);
   w.p1 = (float*)take(Bz * P1 * 4);
@@ -545,7 +552,10 @@ int launch_band6(ba3c_handle* h, hipStream_t s, int kid, const BandArgs& a, cons
       if (ringable && h->ring && a.batch >= pr && (a.batch % pr == 0 || a.batch >= 8 * pr)) {
         // (the forward keeps its double-buffered A fragments and no row prefetch: the
         // no-DBUF layout with the prefetch measured 0.36 -> 0.41 ms, r02ai)
-        hipLaunchKernelGGL(conv_band6r_kernel<L>, dim3(2 * h->cus), dim3(256), 0, s, b);
+        Band6Args br = b;
+        if (h->dynq && a.batch > pr)    // several images per workgroup
+          br.ticket = w.ticket(kid == BA3C_K_CONV1_DGRAD ? TK_C1D : TK_C1F, h);
+        hipLaunchKernelGGL(conv_band6r_kernel<L>, dim3(2 * h->cus), dim3(256), 0, s, br);
         HIP_TRY(hipGetLastError());
         return BA3C_OK;
       }
@@ -611,7 +621,7 @@ WPrep6Args wprep6_args(ba3c_handle* h, const float* prm, const Workspace& w, boo
   pa.wb0 = reinterpret_cast<uint4*>(w.wt + WT_C0S);
   pa.relu = train ? w.relu : nullptr;
   pa.amax = w.amax;
-  pa.n_amax = AMAX_N * (1 + h->cfg.max_batch);
+  pa.n_amax = AMAX_N * (1 + h->cfg.max_batch) + TK_N;   // the tickets too
   pa.wexp = w.wexp;
   return pa;
 }
@@ -1241,10 +1251,10 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   static const Switch kSwitches[] = {{"BA3C_GENERIC", 0, 1},  {"BA3C_C1PAIR", 0, 2},   {"BA3C_SCALARS_RIDE", 0, 1},
                                      {"BA3C_OVERLAP", 0, 2},  {"BA3C_MULTI", 0, 1},    {"BA3C_MULTI_BIG", 0, 3},
                                      {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}, {"BA3C_CHAIN", 0, 1},
-                                     {"BA3C_C1D_SPARSE", 0, 1}};
-  constexpr int NSW = 10;
+                                     {"BA3C_C1D_SPARSE", 0, 1}, {"BA3C_DYNQ", 0, 1}};
+  constexpr int NSW = 11;
   int sw[NSW];
-  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1, 0};
+  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1, 0, 1};
   for (int i = 0; i < NSW; ++i) {
     sw[i] = defaults[i];
     const char* e = getenv(kSwitches[i].name);
@@ -1266,6 +1276,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   h->ring = sw[7] != 0;
   h->chain_on = sw[8] != 0;
   h->c1s = sw[9] != 0;
+  h->dynq = sw[10] != 0;
   h->g6 = h->band;
   {
     int dev = 0, n = 0;

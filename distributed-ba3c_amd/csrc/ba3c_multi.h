@@ -38,9 +38,10 @@ template <class L>
 struct Band6RJob {
   using Args = Band6Args;
   static constexpr int LDS = L::LDS_BYTES;
-  __device__ static void run(const Args& a, int x, int, int, int gx, char* lds, uint32_t*) {
-    if constexpr (L::G::SRC == 1 && L::NS == 2) band6r_up_body<L>(a, x, gx, lds);
-    else band6r_body<L>(a, x, gx, lds);
+  __device__ static void run(const Args& a, int x, int, int, int gx, char* lds, uint32_t* red4) {
+    int* tslot = reinterpret_cast<int*>(red4);   // the ticket slot (dynamic queue only)
+    if constexpr (L::G::SRC == 1 && L::NS == 2) band6r_up_body<L>(a, x, gx, lds, tslot);
+    else band6r_body<L>(a, x, gx, lds, tslot);
   }
 };
 

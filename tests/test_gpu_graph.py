@@ -159,6 +159,39 @@ def test_ring_walk_band_kernels_match_one_band_kernels(monkeypatch):
         assert torch.equal(out[0][2][n], out[1][2][n]), n
 
 
+def test_ring_walk_dynamic_image_queue_matches_static_ranges(monkeypatch):
+    """At the bench's B=2048 (8 x CUs: four images per ring-walk workgroup) conv1's forward and
+    input gradient draw their images from a dynamic queue (one agent-scope ticket per image,
+    BA3C_DYNQ=1, the default) instead of static contiguous ranges (BA3C_DYNQ=0): activations,
+    argmax codes, dp0, every gradient and the scalars bit for bit equal, over two steps (the
+    tickets are re-zeroed by each step's weight-prep launch), and the predictor forward too."""
+    from ba3c_amd.engine import Ba3cEngine
+    B = 8 * torch.cuda.get_device_properties(0).multi_processor_count
+    rs = np.random.RandomState(91)
+    state = torch.from_numpy(rs.randint(0, 256, size=(B, 84, 84, 4)).astype(np.uint8)).cuda()
+    action = torch.from_numpy(rs.randint(0, 4, size=B).astype(np.int64)).cuda()
+    R = torch.from_numpy(rs.normal(size=B).astype(np.float32)).cuda()
+    params = O.init_params(512, 1, 4, seed=21, dtype=np.float32)
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("BA3C_DYNQ", env)
+        eng = Ba3cEngine(num_actions=4, fc_neurons=512, fc_splits=1, max_batch=B)
+        eng.load_params(params)
+        got = []
+        for _ in range(2):
+            sc = eng.train_grads(state, action, R)
+            got.append(eng.grads.clone())
+            got.append(sc.clone())
+        got += [eng.workspace_tensor(n, B).clone() for n in ("p1", "c1", "dp0", "dp1")]
+        got += [t.clone() for t in eng.forward(state)]
+        torch.cuda.synchronize()
+        assert eng.device_errors() == 0
+        out.append(got)
+        del eng
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("frames", ["random", "atari"])
 def test_sparse_conv1_input_gradient_matches_dense(monkeypatch, frames):
     """conv1's input gradient on 2:4-sparse MFMA (ba3c_dgrad1s.h, BA3C_C1D_SPARSE=1, used from
