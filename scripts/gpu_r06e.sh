@@ -6,7 +6,7 @@ T=${1:-r06e}
 mkdir -p gpurun_out/$T
 S=scripts/gpu_step.sh
 Q="--no-cpu-baseline --no-overlap --no-b32"
-$S 900 gpurun_out/$T/pytest_x.log python -u -m pytest -x -v --timeout 240 --timeout-method thread \
+$S 900 gpurun_out/$T/pytest_x.log python -u -m pytest -x -v -s --timeout 300 --timeout-method thread \
   tests/test_gpu_graph.py tests/test_gpu_switches.py tests/test_gpu_hard_inputs.py tests/test_gpu_bench_path.py tests/test_gpu_replicas.py || exit $?
 grep -E "passed|failed" gpurun_out/$T/pytest_x.log | tail -1
 for D in 1 0 1 0; do
