@@ -275,10 +275,13 @@ def time_graph_steps(tr, batch, steps, warmup):
     return time.perf_counter() - t0
 
 
-def overlap_bench(tr, batch, pred_batch, iters, world):
+def overlap_bench(tr, batch, pred_batch, iters, world, masks=(64, 128)):
     """configs[4]: predictor forward of `pred_batch` simulator states on a second HIP stream
     beside the train step.  The predictor engine reads a parameter snapshot taken at the start
-    of each iteration (stricter than the reference's Hogwild reads)."""
+    of each iteration (stricter than the reference's Hogwild reads).  Both sides
+    fill every CU, so the predictor can only gain where the learner leaves CUs idle; `masks`:
+    the same with the predictor's stream restricted to that many CUs (CuMaskedStream), so its
+    workgroups cannot displace the learner's on the other CUs."""
     from ba3c_amd.engine import Ba3cEngine
     eng = tr.engine
     pe = Ba3cEngine(num_actions=eng.num_actions, channels=eng.channels,
@@ -289,12 +292,13 @@ def overlap_bench(tr, batch, pred_batch, iters, world):
                            device="cuda", generator=g)
     ps = torch.cuda.Stream()
     main = torch.cuda.current_stream()
+    masked = {k: hipevent.CuMaskedStream(k) for k in masks}
 
     def pred_only():
         pe.params.copy_(eng.params)
         pe.forward(states)
 
-    def run(mode, n):
+    def run(mode, n, ps=ps):
         sync_all(world)
         t0 = time.perf_counter()
         for _ in range(n):
@@ -321,12 +325,18 @@ def overlap_bench(tr, batch, pred_batch, iters, world):
     t_train = run("train", iters)
     t_pred = run("pred", iters)
     t_both = run("both", iters)
+    part = {}
+    for k, ms in masked.items():
+        run("both", 2, ms.stream)
+        part["predictor_on_%d_cus" % k] = round(run("both", iters, ms.stream), 4)
     B = batch[0].shape[0]
     return {"config": "configs[4]: predictor forward of %d states/GPU + train step (B=%d) on "
                       "separate HIP streams" % (pred_batch, B),
             "train_ms": round(t_train, 4), "predict_ms": round(t_pred, 4),
             "overlapped_ms": round(t_both, 4),
             "overlap_speedup": round((t_train + t_pred) / t_both, 3),
+            "cu_masked_overlapped_ms": part,
+            "cu_masked_speedup": {k: round((t_train + t_pred) / v, 3) for k, v in part.items()},
             "predict_states_per_s": round(world * pred_batch / (t_pred / 1000.0), 1)}
 
 

@@ -1,13 +1,16 @@
 """HIP events with explicit fence flags (torch.cuda.Event cannot pass them).
 
-torch.cuda.Event records with HIP's default system-scope release, and on MI355X that release
-writes back the eight XCDs' L2s and invalidates them: each recorded event left a 5-6 us gap in
-the step's kernel timeline (rocprofv3, profiles/r06/).  Timing marks only need the timestamp,
-so `timing_event()` records with hipEventDisableSystemFence.  Stream joins need ordering, not a
-cache flush: every kernel of this path reads and writes device memory only, and HIP's kernel
-dispatch packets already carry the agent-scope acquire / release that orders one kernel's
-stores before a later kernel's loads on any queue, so `join_event()` records with
-hipEventReleaseToDevice (a device-scope release, the scope those kernels need).
+torch.cuda.Event records with HIP's default system-scope release.  Timing marks only need the
+timestamp, so `timing_event()` records with hipEventDisableSystemFence.  Stream joins need
+ordering, not a system-scope flush: every kernel of this path reads and writes device memory
+only, and HIP's kernel dispatch packets already carry the agent-scope acquire / release that
+orders one kernel's stores before a later kernel's loads on any queue, so `join_event()`
+records with hipEventReleaseToDevice.  Measured (profiles/r06/, same box): the world-1 N>1 step
+1.779 -> 1.761 ms with these events for its cross-stream joins; the N=1 step is unchanged.
+What the flags do NOT remove: every event recorded on the learner stream between two of its
+kernels still leaves a 5-6 us gap in the kernel timeline (rocprofv3 traces r06b-d, whatever
+the flags), so the step records as few as it needs and the timing marks stay out of the timed
+steps (bench.py)."""
 
 The library is the HIP runtime torch loaded (torch/lib/libamdhip64.so), the one libba3c.so and
 RCCL resolve to as well, so these events live in the same runtime as torch's streams.
@@ -36,6 +39,9 @@ def _hip():
         lib.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), P, P]
         lib.hipEventDestroy.argtypes = [P]
         lib.hipStreamWaitEvent.argtypes = [P, P, ctypes.c_uint]
+        lib.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(P), ctypes.c_uint32,
+                                                     ctypes.POINTER(ctypes.c_uint32)]
+        lib.hipStreamDestroy.argtypes = [P]
         lib.hipGetErrorString.restype = ctypes.c_char_p
         lib.hipGetErrorString.argtypes = [ctypes.c_int]
         _HIP = lib
@@ -125,3 +131,35 @@ def wait_stream(waiter, other, ev=None):
         ev.wait(waiter)
     else:
         waiter.wait_event(ev)
+
+
+class CuMaskedStream(object):
+    """A HIP stream whose kernels may only use `n_cus` of the device's CUs
+    (hipExtStreamCreateWithCUMask), spread evenly over the CU numbering, as a torch stream
+    (`.stream`, torch.cuda.ExternalStream).  bench.py's configs[4] partition: the predictor's
+    forward on a subset of the CUs beside the learner's step."""
+
+    def __init__(self, n_cus, device=None):
+        dev = torch.device(device or "cuda")
+        total = torch.cuda.get_device_properties(dev).multi_processor_count
+        if not 0 < n_cus <= total:
+            raise ValueError("n_cus must be in [1, %d]" % total)
+        words = (total + 31) // 32
+        mask = (ctypes.c_uint32 * words)()
+        for i in range(n_cus):
+            cu = (i * total) // n_cus
+            mask[cu // 32] |= 1 << (cu % 32)
+        self.n_cus = n_cus
+        self._s = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            _check(_hip().hipExtStreamCreateWithCUMask(ctypes.byref(self._s), words, mask),
+                   "hipExtStreamCreateWithCUMask")
+        self.stream = torch.cuda.ExternalStream(self._s.value, device=dev)
+
+    def __del__(self):
+        try:
+            if self._s:
+                _hip().hipStreamDestroy(self._s)
+                self._s = ctypes.c_void_p()
+        except Exception:
+            pass
