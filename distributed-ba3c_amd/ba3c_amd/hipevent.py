@@ -10,7 +10,7 @@ records with hipEventReleaseToDevice.  Measured (profiles/r06/, same box): the w
 What the flags do NOT remove: every event recorded on the learner stream between two of its
 kernels still leaves a 5-6 us gap in the kernel timeline (rocprofv3 traces r06b-d, whatever
 the flags), so the step records as few as it needs and the timing marks stay out of the timed
-steps (bench.py)."""
+steps (bench.py).
 
 The library is the HIP runtime torch loaded (torch/lib/libamdhip64.so), the one libba3c.so and
 RCCL resolve to as well, so these events live in the same runtime as torch's streams.
