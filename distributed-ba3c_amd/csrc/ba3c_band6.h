@@ -108,8 +108,10 @@ struct Band6Args {
 // the image, so the results equal the static partition's bit for bit; what changes is that a
 // workgroup held off the chip (a collective's workgroups on its CU) no longer leaves its images
 // for the end of the launch.
+// (an increment, not an add: the compiler's atomic optimizer rewrites a uniform-address add into
+// a wave-aggregated one whose result is read back at once, a full vmcnt wait right at the draw)
 __device__ __forceinline__ unsigned draw_ticket(unsigned* t) {
-  return __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_atomic_inc32(t, 0xFFFFFFFFu, __ATOMIC_RELAXED, "agent");
 }
 
 // packed 16-bit halves: 0xFFFF where the half is zero, else 0 (code-mask of the pooled staging)
@@ -549,7 +551,12 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
     const float asc = exp2i(ka), us1 = exp2i(-ka);
     float omax = 0.f;
     unsigned nt = 0;
-    if (dyn && tid == 0) nt = draw_ticket(a.ticket);        // the image after this one
+    // the image after this one, drawn once the scale's load is consumed (the asm pins the
+    // order: a wait for that load at the branch join would otherwise also wait for the draw)
+    if (dyn) {
+      asm volatile("" ::"v"(asc) : "memory");
+      if (tid == 0) nt = draw_ticket(a.ticket);
+    }
     for (int bi = 0; bi < G::NBANDS; ++bi) {
       const int y0 = bi * G::RB;
       const int rows_out = min(G::RB, G::HO - y0);
@@ -700,7 +707,10 @@ __device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int g
     const float asc = exp2i(ka), us1 = exp2i(-ka);
     float omax = 0.f;
     unsigned nt = 0;
-    if (dyn && tid == 0) nt = draw_ticket(a.ticket);        // the image after this one
+    if (dyn) {                                              // the image after this one (as above)
+      asm volatile("" ::"v"(asc) : "memory");
+      if (tid == 0) nt = draw_ticket(a.ticket);
+    }
     int nimg = img + 1;
     for (int bi = 0; bi < G::NBANDS; ++bi) {
       const int y0 = bi * G::RB;
