@@ -102,9 +102,10 @@ struct Band6Args {
 };
 
 // Dynamic image queue of the ring walks (BA3C_DYNQ, default on where a workgroup walks several
-// images): thread 0 draws the next image with one agent-scope atomic when the workgroup STARTS
-// an image and parks it in an LDS slot one band later, so the round trip hides behind the
-// band's work; the workgroup reads it at the image's end.  Every image's outputs depend only on
+// images): workgroup b starts with image b; thread 0 draws each further image (gx + ticket) with
+// one agent-scope atomic when the workgroup STARTS an image and parks it in an LDS slot one
+// band later, so the round trip hides behind the band's work; the workgroup reads it at the
+// image's end.  Every image's outputs depend only on
 // the image, so the results equal the static partition's bit for bit; what changes is that a
 // workgroup held off the chip (a collective's workgroups on its CU) no longer leaves its images
 // for the end of the launch.
@@ -529,10 +530,8 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
   const bool dyn = a.ticket != nullptr;
   const int ipw = (a.batch + gx - 1) / gx;
   int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
-  if (dyn) {
-    if (tid == 0) *tslot = (int)draw_ticket(a.ticket);
-    __syncthreads();
-    img0 = *tslot;
+  if (dyn) {                  // first image bx (no draw: gx simultaneous same-address draws at
+    img0 = bx;                // the start serialise), then images gx + ticket
     img1 = a.batch;
   }
   // PRE (input-gradient layouts, whose registers allow it): the next band's RB new rows are
@@ -611,7 +610,7 @@ __device__ __forceinline__ void band6r_body(const Band6Args& a, int bx, int gx, 
       if (!BA3C_DIAG_NOCOMPUTE) O::compute(a, lds, wave, lane, img, y0, rows_out, us1, us2, pos, omax, [](int) {});
     }
     if (L::NS == 2) amax_publish(a.amax_out, img, omax, lane);
-    img = dyn ? *tslot : img + 1;   // (written at band 1; bands >= 2 put barriers in between)
+    img = dyn ? gx + *tslot : img + 1;   // (written at band 1; bands >= 2 put barriers in between)
   }
   if (G::POOL && a.relu_count) relu_count_add_uniform(a.relu_count, pos, lane);
 }
@@ -643,12 +642,9 @@ __device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int g
   const bool dyn = a.ticket != nullptr;
   const int ipw = (a.batch + gx - 1) / gx;
   int img0 = bx * ipw, img1 = min(a.batch, img0 + ipw);
-  if (dyn) {
-    if (tid == 0) *tslot = (int)draw_ticket(a.ticket);
-    __syncthreads();
-    img0 = *tslot;
+  if (dyn) {                                                // first image bx, then gx + ticket
+    img0 = bx;
     img1 = a.batch;
-    __syncthreads();                                        // before the slot is written again
   }
 
   // pooled rows bi * RB / 2 .. of image img (new rows of band bi: un-pooled rows y0 .. y0 +
@@ -730,7 +726,7 @@ __device__ __forceinline__ void band6r_up_body(const Band6Args& a, int bx, int g
       }
       store_items(pv, pc, asc);
       __syncthreads();
-      if (dyn && bi == 1) nimg = *tslot;
+      if (dyn && bi == 1) nimg = gx + *tslot;
       {
         // prefetch the workgroup's next band (the next image's first band after the last)
         const int nb = bi + 1 < G::NBANDS ? bi + 1 : 0;

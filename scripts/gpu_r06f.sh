@@ -11,7 +11,7 @@ $S 600 gpurun_out/$T/pytest_x.log python -u -m pytest -x -v -s --timeout 300 --t
 grep -E "passed|failed" gpurun_out/$T/pytest_x.log | tail -1
 for D in 1 0 1 0; do
   BA3C_DYNQ=$D $S 300 gpurun_out/$T/n1_d$D.log python bench.py $Q || exit $?
-  grep -h '^{' gpurun_out/$T/n1_d$D.log | sed "s/^/D$D n1 /" | cut -c1-140 >> gpurun_out/$T/lines.txt
+  grep -h '^{' gpurun_out/$T/n1_d$D.log | sed "s/^/D$D n1 /" | cut -c1-2000 >> gpurun_out/$T/lines.txt
   BA3C_DYNQ=$D $S 300 gpurun_out/$T/sync_d$D.log python bench.py $Q --sync-path --occupy 16 || exit $?
   grep -h '^{' gpurun_out/$T/sync_d$D.log | sed "s/^/D$D sync /" >> gpurun_out/$T/lines.txt
 done
