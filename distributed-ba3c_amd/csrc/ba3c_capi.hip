@@ -152,9 +152,13 @@ struct ba3c_handle {
   // weight-fragment stream and its staging, which two workgroups per CU do not hide, cost
   // 0.07 and 0.13 ms)
   bool c1s = false;
-  // ring walks with several images per workgroup draw their images from a dynamic queue
-  // (Band6Args::ticket); BA3C_DYNQ=0: static contiguous ranges.  Bit-identical either way
-  bool dynq = true;
+  // BA3C_DYNQ=1: ring walks with several images per workgroup draw their images after the
+  // first from a dynamic queue (Band6Args::ticket) instead of static contiguous ranges;
+  // bit-identical either way.  Default 0: same-box r06g, the queue costs ~9 us per step with
+  // the chip to itself (conv1 fwd + dgrad), and with 16 CUs held for 50 us by a stand-in for
+  // RCCL (bench --occupy) conv1 dgrad's slowdown is the same 1.08 either way; it only pays when
+  // CUs are held for the whole launch (1.55 -> 1.14)
+  bool dynq = false;
   // ba3c_train_grads_phase(phase 3): the pass's weight-gradient reduction is left pending and
   // the next fused-clip apply on the handle runs it as the signalling job of a chained launch
   // (reduce -> clip + update, one launch fewer); any other entry point launches it first
@@ -1254,7 +1258,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
                                      {"BA3C_C1D_SPARSE", 0, 1}, {"BA3C_DYNQ", 0, 1}};
   constexpr int NSW = 11;
   int sw[NSW];
-  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1, 0, 1};
+  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1, 0, 0};
   for (int i = 0; i < NSW; ++i) {
     sw[i] = defaults[i];
     const char* e = getenv(kSwitches[i].name);

@@ -162,7 +162,7 @@ def test_ring_walk_band_kernels_match_one_band_kernels(monkeypatch):
 def test_ring_walk_dynamic_image_queue_matches_static_ranges(monkeypatch):
     """At the bench's B=2048 (8 x CUs: four images per ring-walk workgroup) conv1's forward and
     input gradient draw their images from a dynamic queue (one agent-scope ticket per image,
-    BA3C_DYNQ=1, the default) instead of static contiguous ranges (BA3C_DYNQ=0): activations,
+    BA3C_DYNQ=1) instead of static contiguous ranges (BA3C_DYNQ=0, the default): activations,
     argmax codes, dp0, every gradient and the scalars bit for bit equal, over two steps (the
     tickets are re-zeroed by each step's weight-prep launch), and the predictor forward too."""
     from ba3c_amd.engine import Ba3cEngine

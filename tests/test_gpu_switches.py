@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 SETTINGS = [("BA3C_GENERIC", "1"), ("BA3C_C1PAIR", "0"), ("BA3C_C1PAIR", "1"),
             ("BA3C_SCALARS_RIDE", "0"), ("BA3C_OVERLAP", "0"), ("BA3C_OVERLAP", "1"),
             ("BA3C_MULTI", "0"), ("BA3C_MULTI_BIG", "0"), ("BA3C_FUSED_UPDATE", "0"),
-            ("BA3C_RING", "0"), ("BA3C_DYNQ", "0"), (None, None)]
+            ("BA3C_RING", "0"), ("BA3C_DYNQ", "1"), (None, None)]
 GEOM = {32: dict(A=4, C=4, F=128, S=4), 160: dict(A=4, C=4, F=512, S=1)}
 _REF = {}
 
