@@ -186,12 +186,15 @@ def test_sync_replicas_rccl_allreduce_world1_equals_single_replica_step(monkeypa
     np.testing.assert_array_equal(got, ref)
 
 
-def test_configs4_predictor_stream_beside_train_step_equals_serial():
+@pytest.mark.parametrize("cu_mask", [None, 64])
+def test_configs4_predictor_stream_beside_train_step_equals_serial(cu_mask):
     """configs[4] on one GPU: the learner (B=2048, F=512) and an 8192-state predictor forward
-    on a second HIP stream reading a parameter snapshot taken on the learner stream.  The
-    overlapped predictor outputs equal a serial forward on that snapshot bit for bit, the
+    on a second HIP stream reading a parameter snapshot taken on the learner stream (cu_mask:
+    that stream restricted to 64 CUs, hipevent.CuMaskedStream, bench.py's partition variant).
+    The overlapped predictor outputs equal a serial forward on that snapshot bit for bit, the
     learner's parameters equal a serial learner step's, and a 16-state slice matches the
     oracle."""
+    from ba3c_amd import hipevent
     from ba3c_amd.engine import Ba3cEngine
     from ba3c_amd.model import Model
     from ba3c_amd.optimizer import AdamOptimizer
@@ -218,7 +221,8 @@ def test_configs4_predictor_stream_beside_train_step_equals_serial():
 
     tr = learner()
     tr.train_step(state, action, R)
-    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    masked = hipevent.CuMaskedStream(cu_mask) if cu_mask else None
+    main, side = torch.cuda.current_stream(), (masked.stream if masked else torch.cuda.Stream())
     pe.params.copy_(tr.engine.params)            # snapshot on the learner stream
     ev = torch.cuda.Event()
     ev.record(main)
