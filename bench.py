@@ -456,12 +456,16 @@ def exchange_report(tr, batch, iters, world, occupy=(), occupy_us=50.0):
             "rccl_comms": rccl_comms}
 
 
-def find_dominant_kernel(tr, batch, steps=3):
+def find_dominant_kernel(tr, batch, steps=5, warm=20):
     """Probe every kernel id over `steps` steps: (the id with the longest launch time per
     step, {id: ms per step}).  A multi-job launch is timed under its job 0's id; the other
-    jobs' ids read 0 (ba3c_kernel_merged lists them)."""
+    jobs' ids read 0 (ba3c_kernel_merged lists them).  `warm` steps first: the clock is still
+    ramping over the first steps after start (r06b: conv0 and conv1's forward, the first ids
+    probed, read 46 and 58 us above their rocprofv3 medians after 2 warm steps)."""
     from ba3c_amd._lib import KERNEL_IDS
     eng = tr.engine
+    for _ in range(warm):
+        tr.train_step(*batch)
     best, best_ms, per = None, -1.0, {}
     for name in KERNEL_IDS:
         eng.probe_enable(name)
