@@ -34,6 +34,15 @@ __device__ __forceinline__ uint2 lds_tr16(const char* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// packed 16-bit halves: 0xFFFF where the half is zero, else 0
+__device__ __forceinline__ uint32_t w6_mask16_eq0(uint32_t d) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  u16x2 x = __builtin_bit_cast(u16x2, d);
+  x = __builtin_elementwise_min(x, (u16x2){1, 1});
+  x = x + (u16x2){0xFFFF, 0xFFFF};
+  return __builtin_bit_cast(uint32_t, x);
+}
+
 template <int HS_, int WS_, int CIN_, int COUT_, int RB_, int CW_, int OW_, int PX_, int PY_, int NS_ = 3>
 struct Wg6Geom {
   static constexpr int NS = NS_;                          // split planes (3 bf16 / 2 fp16)
@@ -104,10 +113,25 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
   constexpr int XN = G::XROWS * G::WS * XQ;
   constexpr int XPT = (XN + 255) / 256;
   constexpr int YQ = G::OW / 4;                           // float4 per dY pixel (8)
-  constexpr int YN = G::KPAD * YQ;
+  // UNP (BA3C_W6_UNPOOL, default): dY staged per POOLED element — each (pooled pixel, 4
+  // channels) of dP is loaded and split once and written to the four pixels of its window
+  // under per-channel code masks (as wgrad6s / band6r_up): a quarter of the loads and splits,
+  // and 5 float4 + 5 code registers per thread fewer held through the k-loop (conv2's pair
+  // launch spilled 20 B/lane at 256 VGPRs).  The staged LDS image is the per-pixel one bit for
+  // bit (a masked split of v is the split of the masked v; the padded pixels KP .. KPAD - 1 are
+  // zeroed once and never written again)
+#ifndef BA3C_W6_UNPOOL
+#define BA3C_W6_UNPOOL 1
+#endif
+  constexpr bool UNP = BA3C_W6_UNPOOL && G::HO % G::RB == 0 && G::RB % 2 == 0;
+  constexpr int YN = UNP ? (G::RB / 2) * G::PW * YQ : G::KPAD * YQ;
   constexpr int YPT = (YN + 255) / 256;
   float4 xv[XPT], yv[YPT];
   uint32_t yc[YPT];                                       // (un-loaded: dY is zero)
+  if constexpr (UNP) {
+    for (int i = tid; i < (G::KPAD - G::KP) * G::PY / 16; i += 256)
+      reinterpret_cast<uint4*>(ys + G::KP * G::PY)[i] = make_uint4(0, 0, 0, 0);
+  }
 
   const int nbands = a.batch * G::NBANDS;
   // band walk: whole images per workgroup (ring reuse of the halo rows) when the images split
@@ -142,6 +166,19 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
       // compiler wait for every outstanding load at the join, serialising the prefetch
       const bool ok = f < xn && y < G::HS;
       xv[i] = ld4(a.x + (ok ? ((size_t)(img * G::HS + y) * G::WS + x) * G::CIN + c0 + cq * 4 : 0), ok);
+    }
+    if constexpr (UNP) {
+#pragma unroll
+      for (int i = 0; i < YPT; ++i) {
+        const int f = tid + 256 * i;
+        const int oq = f % YQ, rest = f / YQ;
+        const int pc = rest % G::PW, py = (y0 >> 1) + rest / G::PW;
+        const bool ok = f < YN;
+        const size_t e = ok ? ((size_t)(img * G::PH + py) * G::PW + pc) * G::COUT + o0 + oq * 4 : 0;
+        yv[i] = ld4(a.dp + e, ok);
+        yc[i] = ld_u8x4(a.code + e, ok);
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < YPT; ++i) {
@@ -181,6 +218,32 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
             *reinterpret_cast<uint2*>(q + sp * G::XSB) = make_uint2(s0[sp], s1[sp]);
         }
       }
+    }
+    if constexpr (UNP) {
+#pragma unroll
+      for (int i = 0; i < YPT; ++i) {
+        const int f = tid + 256 * i;
+        if (f < YN) {
+          const int oq = f % YQ, rest = f / YQ;
+          const int pc = rest % G::PW, pr = rest / G::PW;
+          uint32_t s0[G::NS], s1[G::NS];
+          SP::split(yv[i].x, yv[i].y, ysc, s0);
+          SP::split(yv[i].z, yv[i].w, ysc, s1);
+          const uint32_t c01 = __builtin_amdgcn_perm(yc[i], yc[i], 0x0C010C00u);   // codes as halves
+          const uint32_t c23 = __builtin_amdgcn_perm(yc[i], yc[i], 0x0C030C02u);
+          char* base = ys + ((2 * pr) * G::WO + 2 * pc) * G::PY + oq * 8;
+#pragma unroll
+          for (int sub = 0; sub < 4; ++sub) {
+            const uint32_t S = (uint32_t)sub * 0x00010001u;
+            const uint32_t m01 = w6_mask16_eq0(c01 ^ S), m23 = w6_mask16_eq0(c23 ^ S);
+            char* d = base + ((sub >> 1) * G::WO + (sub & 1)) * G::PY;
+#pragma unroll
+            for (int sp = 0; sp < G::NS; ++sp)
+              *reinterpret_cast<uint2*>(d + sp * G::YSB) = make_uint2(s0[sp] & m01, s1[sp] & m23);
+          }
+        }
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < YPT; ++i) {
@@ -311,14 +374,6 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
 // both 16-channel c-blocks x both 16-column n-blocks.  Per output the accumulation runs over
 // the same k-steps in the same order as wgrad6_body's (bands in order, 32 permuted pixels per
 // k-step); only the grouping of images into slabs differs.
-// packed 16-bit halves: 0xFFFF where the half is zero, else 0
-__device__ __forceinline__ uint32_t w6_mask16_eq0(uint32_t d) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  u16x2 x = __builtin_bit_cast(u16x2, d);
-  x = __builtin_elementwise_min(x, (u16x2){1, 1});
-  x = x + (u16x2){0xFFFF, 0xFFFF};
-  return __builtin_bit_cast(uint32_t, x);
-}
 
 template <int HS_, int WS_, int CIN_, int COUT_, int RB_, int PX_, int PY_>
 struct Wg6WGeom {
