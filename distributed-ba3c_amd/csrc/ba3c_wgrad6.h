@@ -855,14 +855,20 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
     reinterpret_cast<uint32_t*>(yq)[row * G::QS + Q] = 0u;
     if (row < G::COUT) yi[row * G::QS + Q] = (uint8_t)(2u << 2);
   }
+  // BA3C_W6S_XPF (A/B): 1 = the next band's new X rows are loaded into registers before this
+  // band's k-steps (held through them); 0 = loaded at the start of the band's staging
+#ifndef BA3C_W6S_XPF
+#define BA3C_W6S_XPF 1
+#endif
   int band = img0 * G::NBANDS;
   if (band < band_end) {
-    load_x(img0, G::HALO, xv);
+    if (BA3C_W6S_XPF) load_x(img0, G::HALO, xv);
     load_y(img0, 0);
   }
   for (; band < band_end; ++band) {
     const int img = band / G::NBANDS;
     const int bi = band - img * G::NBANDS;
+    if (!BA3C_W6S_XPF && BA3C_DIAG_W6S != 1) load_x(img, bi * G::RB + G::HALO, xv);
     __syncthreads();                                      // previous band's LDS reads are done
     if (BA3C_DIAG_W6S != 1 && bi > 0) {
       constexpr int N16 = G::HALO * G::WS * G::PX / 16;
@@ -882,7 +888,7 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
     __syncthreads();
     if (BA3C_DIAG_W6S != 1 && band + 1 < band_end) {
       const int ni = (band + 1) / G::NBANDS, nbi = band + 1 - ni * G::NBANDS;
-      load_x(ni, nbi * G::RB + G::HALO, xv);
+      if (BA3C_W6S_XPF) load_x(ni, nbi * G::RB + G::HALO, xv);
       load_y(ni, nbi);
     }
     if (BA3C_DIAG_W6S == 2) continue;
