@@ -1039,7 +1039,6 @@ __global__ void __launch_bounds__(256) sample_kernel(const float* __restrict__ p
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n >= B) return;
   const float* pn = probs + (size_t)n * A;
-  double cdf[MAXA];
   double cum = 0.0;
   int bad = 0;
   for (int k = 0; k < A; ++k) {
@@ -1047,13 +1046,18 @@ __global__ void __launch_bounds__(256) sample_kernel(const float* __restrict__ p
     if (!isfinite(pk)) bad |= 1;
     if (pk < 0.f) bad |= 4;
     cum += (double)pk;
-    cdf[k] = cum;
   }
   if (fabs(cum - 1.0) > 3.4526698300124393e-04) bad |= 2;
-  const double tot = cdf[A - 1];
+  const double tot = cum;
   const double un = u[n];
+  // the cumulative sums again, in the same order (the same doubles as a stored cdf array,
+  // which a runtime A put in scratch memory)
   int64_t a = 0;
-  for (int k = 0; k < A; ++k) a += (cdf[k] / tot <= un) ? 1 : 0;
+  double c = 0.0;
+  for (int k = 0; k < A; ++k) {
+    c += (double)pn[k];
+    a += (c / tot <= un) ? 1 : 0;
+  }
   actions[n] = a;
   if (bad && flag) atomicOr(flag, bad);
 }

@@ -855,10 +855,13 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
     reinterpret_cast<uint32_t*>(yq)[row * G::QS + Q] = 0u;
     if (row < G::COUT) yi[row * G::QS + Q] = (uint8_t)(2u << 2);
   }
-  // BA3C_W6S_XPF (A/B): 1 = the next band's new X rows are loaded into registers before this
-  // band's k-steps (held through them); 0 = loaded at the start of the band's staging
+  // BA3C_W6S_XPF: 1 = the next band's new X rows are loaded into registers before this band's
+  // k-steps and held through them; 0 (default) = loaded at the start of the band's staging.
+  // Holding them put the pair kernel at 256 VGPRs with 44 B/lane of scratch (loop constants
+  // spilled and reloaded in every band's staging); the exposed load is hidden by the conv0
+  // workgroup beside it: same-box r06j, pair 0.4218 -> 0.3928 ms, step 1.739 -> 1.712 ms
 #ifndef BA3C_W6S_XPF
-#define BA3C_W6S_XPF 1
+#define BA3C_W6S_XPF 0
 #endif
   int band = img0 * G::NBANDS;
   if (band < band_end) {
