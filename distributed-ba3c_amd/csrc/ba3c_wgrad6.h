@@ -863,6 +863,11 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
 #ifndef BA3C_W6S_XPF
 #define BA3C_W6S_XPF 0
 #endif
+  // BA3C_W6S_APF (A/B): 1 (default) = the next k-step's A words and index nibbles are read
+  // during the last unit of a k-step; 0 = at the k-step's end (16 + 2 fewer live VGPRs)
+#ifndef BA3C_W6S_APF
+#define BA3C_W6S_APF 1
+#endif
   int band = img0 * G::NBANDS;
   if (band < band_end) {
     if (BA3C_W6S_XPF) load_x(img0, G::HALO, xv);
@@ -950,7 +955,7 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
           read_b(u + 1, xq, bb[(u + 1) & 1]);
         } else if (PF) {
           addr(s + 1, xn);
-          read_a(s + 1, avn, ixn);
+          if (BA3C_W6S_APF) read_a(s + 1, avn, ixn);
           read_b(0, xn, bb[NU & 1]);
         }
         __builtin_amdgcn_sched_barrier(0);                // keep those reads ahead of the MFMAs
@@ -972,11 +977,15 @@ __device__ __forceinline__ void wgrad6s_units(const Wg6Args& a, int bx, int gx, 
                 __builtin_bit_cast(f16x8, av[m][pr == 2 ? 1 : 0]), b16[pr == 1 ? 1 : 0], acc[u][m], (int)ix[m], 0, 0);
       }
       if (PF) {
+        if (BA3C_W6S_APF) {
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          av[m][0] = avn[m][0];
-          av[m][1] = avn[m][1];
-          ix[m] = ixn[m];
+          for (int m = 0; m < 2; ++m) {
+            av[m][0] = avn[m][0];
+            av[m][1] = avn[m][1];
+            ix[m] = ixn[m];
+          }
+        } else {
+          read_a(s + 1, av, ix);                          // (not prefetched: read here)
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) xq[r] = xn[r];
