@@ -79,6 +79,11 @@ def load():
         "ba3c_set_phase2_event": (i32, [P, P]),
         "ba3c_clip_grads_range2": (i32, [P, P, P, P, i32, i32, i32]),
         "ba3c_occupy_cus": (i32, [P, i32, ctypes.c_double]),
+        "ba3c_comm_unique_id": (i32, [P]),
+        "ba3c_comm_init": (i32, [P, P, i32, i32]),
+        "ba3c_comm_destroy": (i32, [P, i32]),
+        "ba3c_allreduce_sum": (i32, [P, P, P, i64]),
+        "ba3c_allreduce_mean": (i32, [P, P, P, i64]),
         "ba3c_apply_update": (i32, [P, P, i32, P, P, P, P, ctypes.POINTER(Ba3cOptParams), f32,
                                     i32, P]),
         "ba3c_apply_update_dev": (i32, [P, P, i32, P, P, P, P, ctypes.POINTER(Ba3cOptParams), P,

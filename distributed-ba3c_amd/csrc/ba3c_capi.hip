@@ -7,6 +7,8 @@
 //   and input gradients (MFMA dgrad with MaxPoolGrad/ReluGrad fused into the loaders).
 // No device allocation and no synchronisation happen inside any entry point.
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>   // types only: the functions are resolved from the loaded RCCL (dlsym)
 
 #include <cmath>
 #include <cstdio>
@@ -181,6 +183,9 @@ struct ba3c_handle {
   // weight-gradient reductions of the running backward pass, launched together at its end
   bool defer_reduce = false;
   ReduceJobs rjobs{};
+  // RCCL communicator of the C-ABI gradient exchange (ba3c_comm_init; null: none)
+  ncclComm_t comm = nullptr;
+  int comm_ranks = 0;
   // timing probe
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
@@ -1227,6 +1232,39 @@ bool check_ptr(const void* p) { return p != nullptr && (reinterpret_cast<uintptr
 
 }  // namespace
 
+namespace {
+struct Rccl {
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                             hipStream_t) = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*abort)(ncclComm_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!lib) lib = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!lib) return x;
+    x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(dlsym(lib, "ncclGetUniqueId"));
+    x.init_rank = reinterpret_cast<decltype(x.init_rank)>(dlsym(lib, "ncclCommInitRank"));
+    x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(lib, "ncclAllReduce"));
+    x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(lib, "ncclCommDestroy"));
+    x.abort = reinterpret_cast<decltype(x.abort)>(dlsym(lib, "ncclCommAbort"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(lib, "ncclGetErrorString"));
+    x.ok = x.get_unique_id && x.init_rank && x.all_reduce && x.destroy && x.abort && x.error_string;
+    return x;
+  }();
+  return r;
+}
+int rccl_fail(ncclResult_t e, const char* what) {
+  return fail(BA3C_ERR_HIP, std::string(what) + ": " + rccl().error_string(e));
+}
+}  // namespace
+
 // =========================================================================================
 extern "C" {
 
@@ -1367,8 +1405,11 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   return BA3C_OK;
 }
 
+int ba3c_comm_destroy(ba3c_handle* h, int32_t abort);
+
 void ba3c_destroy(ba3c_handle* h) {
   if (!h) return;
+  if (h->comm) (void)ba3c_comm_destroy(h, 0);
   for (auto e : h->ev_begin) (void)hipEventDestroy(e);
   for (auto e : h->ev_end) (void)hipEventDestroy(e);
   for (auto e : h->ev_fork)
@@ -1908,6 +1949,69 @@ int ba3c_occupy_cus(void* stream, int32_t n_cus, double usec) {
   if (n_cus == 0 || usec == 0.0) return BA3C_OK;
   hipLaunchKernelGGL(occupy_kernel, dim3(n_cus), dim3(64), 0, static_cast<hipStream_t>(stream),
                      (unsigned long long)(usec * 100.0));   // 100 MHz realtime clock
+  HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+// ---- gradient exchange through the C ABI ----------
+// RCCL is resolved at run time from the library already loaded in the process (torch's copy,
+// or /opt/rocm's librccl.so.1 for a caller without torch): both carry the soname
+// librccl.so.1, so one RCCL serves torch.distributed and these entry points.
+
+int ba3c_comm_unique_id(void* id_out) {
+  if (!id_out) return fail(BA3C_ERR_INVALID, "null argument");
+  if (!rccl().ok) return fail(BA3C_ERR_HIP, "RCCL (librccl.so.1) not found");
+  ncclUniqueId id;
+  const ncclResult_t e = rccl().get_unique_id(&id);
+  if (e != ncclSuccess) return rccl_fail(e, "ncclGetUniqueId");
+  std::memcpy(id_out, &id, sizeof(id));
+  return BA3C_OK;
+}
+
+int ba3c_comm_init(ba3c_handle* h, const void* id, int32_t nranks, int32_t rank) {
+  if (!h || !id) return fail(BA3C_ERR_INVALID, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(BA3C_ERR_INVALID, "bad rank / rank count");
+  if (h->comm) return fail(BA3C_ERR_INVALID, "the handle already has a communicator");
+  if (!rccl().ok) return fail(BA3C_ERR_HIP, "RCCL (librccl.so.1) not found");
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  const ncclResult_t e = rccl().init_rank(&h->comm, nranks, uid, rank);
+  if (e != ncclSuccess) {
+    h->comm = nullptr;
+    return rccl_fail(e, "ncclCommInitRank");
+  }
+  h->comm_ranks = nranks;
+  return BA3C_OK;
+}
+
+int ba3c_comm_destroy(ba3c_handle* h, int32_t abort) {
+  if (!h) return fail(BA3C_ERR_INVALID, "null handle");
+  if (!h->comm) return BA3C_OK;
+  const ncclResult_t e = abort ? rccl().abort(h->comm) : rccl().destroy(h->comm);
+  h->comm = nullptr;
+  h->comm_ranks = 0;
+  if (e != ncclSuccess) return rccl_fail(e, abort ? "ncclCommAbort" : "ncclCommDestroy");
+  return BA3C_OK;
+}
+
+int ba3c_allreduce_sum(ba3c_handle* h, void* stream, float* buf, int64_t count) {
+  if (!h || !buf || count < 0) return fail(BA3C_ERR_INVALID, "bad argument");
+  if (!h->comm) return fail(BA3C_ERR_INVALID, "no communicator (ba3c_comm_init)");
+  CHECK(flush_reduce(h, static_cast<hipStream_t>(stream)));
+  CHECK(flush_held(h, static_cast<hipStream_t>(stream)));
+  const ncclResult_t e = rccl().all_reduce(buf, buf, (size_t)count, ncclFloat32, ncclSum, h->comm,
+                                           static_cast<hipStream_t>(stream));
+  if (e != ncclSuccess) return rccl_fail(e, "ncclAllReduce");
+  return BA3C_OK;
+}
+
+int ba3c_allreduce_mean(ba3c_handle* h, void* stream, float* grads, int64_t count) {
+  if (!check_ptr(grads)) return fail(BA3C_ERR_INVALID, "null or misaligned pointer");
+  CHECK(ba3c_allreduce_sum(h, stream, grads, count));
+  if (h->comm_ranks == 1 || count == 0) return BA3C_OK;   // x / 1 == x
+  const float inv = 1.0f / (float)h->comm_ranks;
+  hipLaunchKernelGGL(scale_kernel, dim3((unsigned)std::min<int64_t>((count + 1023) / 1024, 4096)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), grads, count, inv);
   HIP_TRY(hipGetLastError());
   return BA3C_OK;
 }

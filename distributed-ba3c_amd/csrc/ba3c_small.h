@@ -1018,6 +1018,18 @@ __global__ void __launch_bounds__(256) clip_range_kernel(float* __restrict__ g, 
 // a = searchsorted(cdf, u, 'right').  flag bits: 1 non-finite p (train.py:381), 2 |sum-1| >
 // sqrt(eps_f32) ("probabilities do not sum to 1"), 4 negative p.
 // ---------------------------------------------------------------------------------------
+// ba3c_allreduce_mean: the summed gradients times 1/N (grid-stride, float4 where aligned)
+__global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ g, int64_t n, float s) {
+  const int64_t n4 = n / 4;
+  float4* g4 = reinterpret_cast<float4*>(g);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 v = g4[i];
+    v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+    g4[i] = v;
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) g[i] *= s;
+}
+
 // Diagnostic (ba3c_occupy_cus): each workgroup declares the whole 160 KiB of a CU's LDS, so
 // `n` workgroups hold `n` distinct CUs against every kernel that uses LDS (all the conv
 // kernels) for `ticks` of the 100 MHz realtime clock — a stand-in for RCCL's channel

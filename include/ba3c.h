@@ -242,6 +242,22 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags);
 
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
+/* The synchronous gradient exchange through the C ABI (SURVEY.md §8b `ba3c_allreduce_mean`;
+ * replaces the SyncReplicasOptimizer aggregation on the parameter servers,
+ * OpenAIGym/train.py:598-606): an RCCL communicator owned by the handle.  RCCL is resolved at
+ * run time from the process's librccl.so.1 (torch's copy when torch is loaded).
+ * ba3c_comm_unique_id: rank 0 draws BA3C_UNIQUE_ID_BYTES bytes and the caller broadcasts them;
+ * ba3c_comm_init is collective over the ranks; ba3c_comm_destroy(abort = 1) does not wait for
+ * enqueued collectives (an exit path where a peer may be gone).  ba3c_allreduce_sum sums
+ * `count` floats in place over the ranks on `stream`; ba3c_allreduce_mean also scales them by
+ * 1/nranks (16-byte aligned `grads`).  The Python trainer drives the same RCCL through
+ * ba3c_amd/rccl.py, with the same semantics. */
+#define BA3C_UNIQUE_ID_BYTES 128
+int ba3c_comm_unique_id(void* id_out);
+int ba3c_comm_init(ba3c_handle* h, const void* id, int32_t nranks, int32_t rank);
+int ba3c_comm_destroy(ba3c_handle* h, int32_t abort);
+int ba3c_allreduce_sum(ba3c_handle* h, void* stream, float* buf, int64_t count);
+int ba3c_allreduce_mean(ba3c_handle* h, void* stream, float* grads, int64_t count);
 /* Diagnostic, not part of the reference's interface: enqueue on `stream` a launch of `n_cus`
  * workgroups that each hold one whole CU (all 160 KiB of its LDS) for `usec` microseconds,
  * doing nothing.  bench.py --occupy uses it on the exchange stream to stand in for RCCL's

@@ -238,3 +238,32 @@ def test_configs4_predictor_stream_beside_train_step_equals_serial(cu_mask):
     snap = {k: v.astype(np.float64) for k, v in pe.state_dict().items()}
     t = O.get_nn_prediction(snap, sims[4000:4016].cpu().numpy(), {"fc_neurons": 512, "fc_splits": 1})
     assert rel(got[0][4000:4016].cpu().numpy(), t["logits"]) < FWD_TOL
+
+
+def test_cabi_rccl_exchange_world1():
+    """The C-ABI exchange (ba3c_comm_unique_id / ba3c_comm_init / ba3c_allreduce_sum / _mean,
+    SURVEY.md §8b) in a world-1 communicator owned by the handle: the sum of exact small
+    integers is exact, the mean over one rank is the identity, a second init on the same
+    handle is refused, and destroy (plain and abort) leaves the handle usable for a new one."""
+    import ctypes
+    from ba3c_amd import _lib
+    from ba3c_amd.engine import Ba3cEngine
+    eng = Ba3cEngine(num_actions=4, fc_neurons=128, fc_splits=4, max_batch=4)
+    lib = eng.lib
+    uid = ctypes.create_string_buffer(128)
+    _lib.check(lib.ba3c_comm_unique_id(uid))
+    _lib.check(lib.ba3c_comm_init(eng.h, uid, 1, 0))
+    assert lib.ba3c_comm_init(eng.h, uid, 1, 0) != 0          # one communicator per handle
+    n = 100003
+    x = torch.arange(n, dtype=torch.float32, device="cuda")
+    want = x.clone()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(lib.ba3c_allreduce_sum(eng.h, stream, ctypes.c_void_p(x.data_ptr()), n))
+    _lib.check(lib.ba3c_allreduce_mean(eng.h, stream, ctypes.c_void_p(x.data_ptr()), n))
+    torch.cuda.synchronize()
+    assert torch.equal(x, want)
+    _lib.check(lib.ba3c_comm_destroy(eng.h, 0))
+    assert lib.ba3c_allreduce_sum(eng.h, stream, ctypes.c_void_p(x.data_ptr()), n) != 0
+    _lib.check(lib.ba3c_comm_unique_id(uid))
+    _lib.check(lib.ba3c_comm_init(eng.h, uid, 1, 0))
+    _lib.check(lib.ba3c_comm_destroy(eng.h, 1))
