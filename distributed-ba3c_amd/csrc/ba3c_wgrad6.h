@@ -283,8 +283,8 @@ __device__ __forceinline__ void wgrad6_body(const Wg6Args& a, int bx, int by, in
     if (BA3C_DIAG_W6 != 1 && band + bstep < band_end) load_band(band + bstep);
 
 #ifndef BA3C_W6_UNROLL
-#define BA3C_W6_UNROLL 1      // k-steps unrolled per loop iteration (A/B)
-#endif
+#define BA3C_W6_UNROLL 2      // k-steps unrolled per loop iteration: 2 since the pooled staging
+#endif                        // freed the registers (r06l: conv2 pair 0.2157 -> 0.2105 ms; r03: 1 -> 2 spilled)
 #pragma unroll BA3C_W6_UNROLL
     for (int s = 0; s < (BA3C_DIAG_W6 == 2 ? 0 : G::KS); ++s) {
       // this lane's pixel rows for tr reads r = 0, 1

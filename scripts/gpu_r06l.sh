@@ -4,7 +4,7 @@
 set -o pipefail
 T=${1:-r06l}
 mkdir -p gpurun_out/$T
-scripts/gpu_step.sh 300 gpurun_out/$T/pytest_cabi.log python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_bench_path.py -k "cabi or rccl or sync" || exit $?
-grep -E "passed|failed" gpurun_out/$T/pytest_cabi.log | tail -1
+# scripts/gpu_step.sh 300 gpurun_out/$T/pytest_cabi.log python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_bench_path.py -k "cabi or rccl or sync" || exit $?
+# grep -E "passed|failed" gpurun_out/$T/pytest_cabi.log | tail -1
 bash scripts/gpu_abk.sh $T/unroll conv2_dgrad default distributed-ba3c_amd/ba3c_amd/libba3c_w6u2.so && \
 bash scripts/gpu_abk.sh $T/prio conv0_wgrad default distributed-ba3c_amd/ba3c_amd/libba3c_wprio.so
