@@ -66,7 +66,10 @@ int fail(int code, const std::string& msg) {
       return fail(BA3C_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));        \
   } while (0)
 
-constexpr int kWgradTargetBlocks = 1024;
+#ifndef BA3C_WGRAD_TARGET
+#define BA3C_WGRAD_TARGET 1024   // split-K workgroups a GEMM-engine weight gradient aims for (A/B)
+#endif
+constexpr int kWgradTargetBlocks = BA3C_WGRAD_TARGET;
 constexpr int kMaxBatch = 16384;
 
 inline int64_t align64(int64_t x) { return (x + 63) & ~int64_t(63); }
@@ -234,7 +237,10 @@ struct Lay {
 #ifndef BA3C_C2D_PADSKIP
 #define BA3C_C2D_PADSKIP 1
 #endif
-  using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2, false, false, BA3C_C2D_PADSKIP>;
+#ifndef BA3C_C2D_DBUF
+#define BA3C_C2D_DBUF 0
+#endif
+  using C2D = Band6<GConv2DW, 160, 128, 11, 32, 2, BA3C_C2D_DBUF, false, BA3C_C2D_PADSKIP>;
   using C2FS = Band6<GConv2FS, 160, 64, 2, 0, 2, true>;
   using C2DS = Band6<GConv2DS, 160, 128, 2, 32, 2, true>;
   using W1 = Wg6Geom<40, 40, 32, 32, 4, 16, 32, 96, 160, 2>;
