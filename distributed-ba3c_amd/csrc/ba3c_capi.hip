@@ -164,6 +164,12 @@ struct ba3c_handle {
   // RCCL (bench --occupy) conv1 dgrad's slowdown is the same 1.08 either way; it only pays when
   // CUs are held for the whole launch (1.55 -> 1.14)
   bool dynq = false;
+  // BA3C_C3W_RIDE (large batches, conv2's gradients in one multi-job launch): conv3's weight
+  // gradient as a third job of that launch instead of a launch of its own (two 256-thread
+  // workgroups per slab, bit-identical slabs); 1: after conv2's jobs, 2: before them, 0: own
+  // launch (default: r06n, conv2's launch grows by conv3's whole 22 us either way, since both
+  // fill every workgroup slot; the step gains 0-3 us, within box noise)
+  int c3ride = 0;
   // ba3c_train_grads_phase(phase 3): the pass's weight-gradient reduction is left pending and
   // the next fused-clip apply on the handle runs it as the signalling job of a chained launch
   // (reduce -> clip + update, one launch fewer); any other entry point launches it first
@@ -958,6 +964,9 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     mp.dst = grads + h->tensors[h->idx_conv[layer]].offset;
     return launch_reduce(h, ws, part, pl.S, mp);
   };
+  // conv3's weight gradient when it rides on conv2's launch (BA3C_C3W_RIDE)
+  Conv3WArgs c3w{};
+  int c3w_gx = 0;
   // conv3
   {
     WgradPlan pl = plan_wgrad(576, 64, B * 25, 128, 64);
@@ -989,10 +998,13 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
         } else {
           CHECK(launch_conv3<true>(h, s, BA3C_K_CONV3_DGRAD, da));
         }
-        {
+        const Conv3WArgs wa{w.p2, w.dy3, w.part_3, B, w.am(AM_P2, h), w.am(AM_DY3, h), 0};
+        if (mj_c2 && h->c3ride) {
+          c3w = wa;   // a job of conv2's launch below
+          c3w_gx = gx;
+        } else {
           ProbeScope ps(h, s, BA3C_K_CONV3_WGRAD);
-          hipLaunchKernelGGL(conv3_wgrad_kernel, dim3(gx), dim3(512), 0, s,
-                             Conv3WArgs{w.p2, w.dy3, w.part_3, B, w.am(AM_P2, h), w.am(AM_DY3, h), 0});
+          hipLaunchKernelGGL(conv3_wgrad_kernel, dim3(gx), dim3(512), 0, s, wa);
         }
         HIP_TRY(hipGetLastError());
       }
@@ -1022,9 +1034,18 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
     const dim3 wg = wgrad6_grid<typename LY::W2>(W6_P2, B);
     const Band6Args da = band6_args<typename LY::C2D>(h, BandArgs{w.dp2, w.c2, w.wt + WT_C2D, w.dp1, nullptr, nullptr, B},
                                                      w, WT_C2D, SplitIO{AM_DP2, WJ_C2D, AM_DP1});
-    CHECK((launch_multi<true, Band6Job<typename LY::C2D>, Wg6Job<typename LY::W2>>(
-        s, da, dim3(B * LY::C2D::G::NBANDS), wa, wg, 0, dim3(0, 1, 1), h, BA3C_K_CONV2_DGRAD)));
+    const dim3 gd(B * LY::C2D::G::NBANDS), g3(c3w_gx, 2);
+    if (c3w_gx && h->c3ride == 2)
+      CHECK((launch_multi<true, Conv3WJob, Band6Job<typename LY::C2D>, Wg6Job<typename LY::W2>>(
+          s, c3w, g3, da, gd, wa, wg, h, BA3C_K_CONV2_DGRAD)));
+    else if (c3w_gx)
+      CHECK((launch_multi<true, Band6Job<typename LY::C2D>, Wg6Job<typename LY::W2>, Conv3WJob>(
+          s, da, gd, wa, wg, c3w, g3, h, BA3C_K_CONV2_DGRAD)));
+    else
+      CHECK((launch_multi<true, Band6Job<typename LY::C2D>, Wg6Job<typename LY::W2>>(
+          s, da, gd, wa, wg, 0, dim3(0, 1, 1), h, BA3C_K_CONV2_DGRAD)));
     h->merged[BA3C_K_CONV2_DGRAD] |= 1u << BA3C_K_CONV2_WGRAD;
+    if (c3w_gx) h->merged[BA3C_K_CONV2_DGRAD] |= 1u << BA3C_K_CONV3_WGRAD;
     CHECK(reduce_wgrad6<typename LY::W2>(h, s, wa, (int)wg.x, grads + h->tensors[h->idx_conv[2]].offset));
   } else {
     if (h->band) {
@@ -1299,10 +1320,11 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   static const Switch kSwitches[] = {{"BA3C_GENERIC", 0, 1},  {"BA3C_C1PAIR", 0, 2},   {"BA3C_SCALARS_RIDE", 0, 1},
                                      {"BA3C_OVERLAP", 0, 2},  {"BA3C_MULTI", 0, 1},    {"BA3C_MULTI_BIG", 0, 3},
                                      {"BA3C_FUSED_UPDATE", 0, 1}, {"BA3C_RING", 0, 1}, {"BA3C_CHAIN", 0, 1},
-                                     {"BA3C_C1D_SPARSE", 0, 1}, {"BA3C_DYNQ", 0, 1}};
-  constexpr int NSW = 11;
+                                     {"BA3C_C1D_SPARSE", 0, 1}, {"BA3C_DYNQ", 0, 1},
+                                     {"BA3C_C3W_RIDE", 0, 2}};
+  constexpr int NSW = 12;
   int sw[NSW];
-  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1, 0, 0};
+  const int defaults[NSW] = {0, 2, 1, 2, 1, 3, 1, 1, 1, 0, 0, 0};
   for (int i = 0; i < NSW; ++i) {
     sw[i] = defaults[i];
     const char* e = getenv(kSwitches[i].name);
@@ -1325,6 +1347,7 @@ int ba3c_create(const ba3c_config* cfg, ba3c_handle** out) {
   h->chain_on = sw[8] != 0;
   h->c1s = sw[9] != 0;
   h->dynq = sw[10] != 0;
+  h->c3ride = sw[11];
   h->g6 = h->band;
   {
     int dev = 0, n = 0;

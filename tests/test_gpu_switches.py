@@ -1,5 +1,5 @@
 """Every launch-structure switch ba3c_create reads (BA3C_GENERIC, _C1PAIR, _SCALARS_RIDE,
-_OVERLAP, _MULTI, _MULTI_BIG, _FUSED_UPDATE, _RING) held to the oracle: one training pass at
+_OVERLAP, _MULTI, _MULTI_BIG, _FUSED_UPDATE, _RING, _DYNQ, _C3W_RIDE) held to the oracle: one training pass at
 configs[1]'s B=32 (F=128, S=4) and at B=160 (F=512, S=1: the bench geometry above SMALL_B) —
 every gradient within 1e-4 and the TfDictOp scalars against the fp64 oracle driven by the
 run's own discrete decisions (train.py:164-327, multigpu.py:85-86) — then one fused clip + Adam
@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 SETTINGS = [("BA3C_GENERIC", "1"), ("BA3C_C1PAIR", "0"), ("BA3C_C1PAIR", "1"),
             ("BA3C_SCALARS_RIDE", "0"), ("BA3C_OVERLAP", "0"), ("BA3C_OVERLAP", "1"),
             ("BA3C_MULTI", "0"), ("BA3C_MULTI_BIG", "0"), ("BA3C_FUSED_UPDATE", "0"),
-            ("BA3C_RING", "0"), ("BA3C_DYNQ", "1"), (None, None)]
+            ("BA3C_RING", "0"), ("BA3C_DYNQ", "1"), ("BA3C_C3W_RIDE", "1"), ("BA3C_C3W_RIDE", "2"),
+            (None, None)]
 GEOM = {32: dict(A=4, C=4, F=128, S=4), 160: dict(A=4, C=4, F=512, S=1)}
 _REF = {}
 
