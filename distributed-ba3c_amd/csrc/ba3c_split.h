@@ -148,6 +148,9 @@ struct Conv0S {
 #ifndef BA3C_C0F_PIPE
 #define BA3C_C0F_PIPE 1   // chunk c's MFMAs interleaved with chunk c - 1's pool epilogue (two accumulator sets)
 #endif
+#ifndef BA3C_C0F_POSPK
+#define BA3C_C0F_POSPK 1  // ReLU positives by saturating pack + byte gather + popcount (A/B: 0)
+#endif
 #ifndef BA3C_C0F_MCH
 #define BA3C_C0F_MCH (BA3C_C0F_PIPE ? 2 : 5)
 #endif
@@ -244,6 +247,14 @@ struct Conv0SArgs {
 __device__ __forceinline__ int c0w_pos1(int x, int after) {
   int r;
   asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(x), "v"(after));
+  return r;
+}
+
+// max(t, x, 0) in one v_max3_i32; x an MFMA result read after t, a compiler-visible VALU
+// result of the same accumulator (as c0w_pos1)
+__device__ __forceinline__ int c0w_max3z(int t, int x) {
+  int r;
+  asm("v_max3_i32 %0, %1, %2, 0" : "=v"(r) : "v"(t), "v"(x));
   return r;
 }
 
@@ -400,7 +411,7 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
       lb[s][h] = pix0 + (tap / G::KT) * RP + tap % G::KT;
     }
 
-  int pos = 0;                                      // this lane's ReLU positives (TRAIN)
+  int pos = 0;                                      // this lane's ReLU positives (TRAIN; 8x with BA3C_C0F_POSPK)
   // (sum_k u8 * w 2^kw) * (2^-kw / 255): scaling by a power of two commutes with the rounding
   const float oscale = (1.0f / 255.0f) * exp2i(-wx);
   // Epilogue stores go through a wave-private LDS area holding one pooled row of outputs
@@ -462,7 +473,9 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
           const int cofs = 4 * (jj % G::MBROW) * G::COUT + nt * 16;
           const int b0 = __float_as_int(acc[j][nt][0]), b1 = __float_as_int(acc[j][nt][1]);
           const int b2 = __float_as_int(acc[j][nt][2]), b3 = __float_as_int(acc[j][nt][3]);
-          const int m = max(max(max(b0, b1), b2), max(b3, 0));
+          // max3 (b0, b1, b2) then max3 (., b3, 0): two v_max3_i32 (the compiler splits the
+          // second into a max and a max with 0)
+          const int m = c0w_max3z(max(max(b0, b1), b2), b3);
           bmaxi = max(bmaxi, m);
           wst[lane_el + cofs] = __int_as_float(m) * oscale;
           if constexpr (TRAIN) {
@@ -477,7 +490,17 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
             // instructions but measured slower (0.189 -> 0.209 ms, VALU-to-SALU dependencies)
             // (x > 0) as med3(x, 0, 1) on the bits (v_med3_i32) and three-input adds: no VCC
             // round trips (a compare + add-with-carry per value chained the four through VCC)
+#if BA3C_C0F_POSPK
+            // 8 x (positives): v_cvt_pk_i16_i32 saturates the bits of a positive value to
+            // 0x7FFF, of zero to 0, of a negative one to 0x8000, so the low byte of each half is
+            // 0xFF exactly for a positive value; one v_perm_b32 gathers the four low bytes and
+            // v_bcnt_u32_b32 adds 8 per positive (4 VALU per window instead of 6)
+            pos += __builtin_popcount(__builtin_amdgcn_perm(
+                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(b2, b3)),
+                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_i16(b0, b1)), 0x06040200u));
+#else
             pos += (c0w_pos1(b0, m) + c0w_pos1(b1, m)) + (c0w_pos1(b2, m) + c0w_pos1(b3, m));
+#endif
             // materialise the count here: otherwise it is sunk to its only use after the band
             // loop, keeping every accumulator of the chunk live (r03g: > 256 registers)
             asm volatile("" : "+v"(pos));
@@ -542,7 +565,8 @@ __device__ __forceinline__ void conv0s_fwd_body_t(const Conv0SArgs& a, int bx, i
     amax_publish(a.amax_out, img, __int_as_float(bmaxi) * oscale, lane);
   }
   if (!zdone) chain_wait_wave(a.zsig, a.zneed, a.zerr);
-  if (TRAIN && a.relu_count) relu_count_add(a.relu_count, (unsigned long long)pos, lane);
+  if (TRAIN && a.relu_count)
+    relu_count_add(a.relu_count, (unsigned long long)(BA3C_C0F_POSPK ? pos >> 3 : pos), lane);
 }
 
 #if !BA3C_SHARED_KERNELS  // emitted by ba3c_conv0.hip only
