@@ -85,11 +85,23 @@ typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, f16x2v));
 }
-// (a, b) = hi + lo (+ 2^-22 relative), each a packed fp16 pair
+// (a, b) = hi + lo (+ 2^-22 relative), each a packed fp16 pair.  lo = RN_f16(a - hi) with
+// a - hi exact in fp32: v_fma_mixlo_f16 / v_fma_mixhi_f16 take hi's halves as fp16 operands
+// and write the rounded fp16 results into lo's halves, 2 instructions for the pair instead of
+// 2 conversions to fp32 and a packed fma + pack (BA3C_SPLIT_MIX=1).  Bit-identical, but slower:
+// conv1 forward 0.2856 -> 0.2913 ms, conv1 dgrad +3 us (r06q), so the plain form is the default
+#ifndef BA3C_SPLIT_MIX
+#define BA3C_SPLIT_MIX 0
+#endif
 __device__ __forceinline__ void split2x2(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = pack_f16x2(a, b);
+#if BA3C_SPLIT_MIX
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hi), "v"(a));
+  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hi), "v"(b));
+#else
   const f16x2v h = __builtin_bit_cast(f16x2v, hi);
   lo = pack_f16x2(a - (float)h[0], b - (float)h[1]);
+#endif
 }
 __device__ __forceinline__ void split2(float w, uint32_t& hi, uint32_t& lo) {
   uint32_t h2, l2;
