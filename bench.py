@@ -224,17 +224,19 @@ def sync_all(world):
         torch.cuda.synchronize()
 
 
-def time_steps(tr, batch, steps, warmup, world, probe=None):
+def time_steps(tr, batch, steps, warmup, world, probe=None, probe_every=1):
     """Time exactly `steps` steps bracketed by barrier + synchronize (max over ranks): the
     wall clock, and HIP events around the whole run on the learner stream.  Then, outside the
     timed region, `steps` more steps with an event after each (every event recorded on the
     learner stream leaves a 5-6 us gap between its kernels, r06c trace) for the per-step
-    median."""
+    median.  `probe`: the kernel whose launches the HIP-event probe brackets inside the timed
+    steps, the first of every `probe_every` (each bracket's two events leave ~10 us of gaps in
+    the stream, so a throughput run samples them; ba3c_probe_every)."""
     for _ in range(warmup):
         tr.train_step(*batch)
     sync_all(world)
     if probe is not None:
-        tr.engine.probe_enable(probe)   # bracket the dominant kernel over the timed steps only
+        tr.engine.probe_enable(probe, probe_every)   # the dominant kernel, timed steps only
     e0, e1 = hipevent.timing_event(), hipevent.timing_event()   # no system fence (hipevent.py)
     t0 = time.perf_counter()
     e0.record()
@@ -605,6 +607,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
+    # the roofline probe brackets the dominant launch of one timed step in this many (1: every
+    # step; one in 5 measured the same step time, r06s)
+    ap.add_argument("--probe-every", type=int, default=1)
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--fc_neurons", type=int, default=512)
     ap.add_argument("--fc_splits", type=int, default=1)
@@ -670,7 +675,7 @@ def run_rank(args, world, rank, local):
     sync_all(world)
 
     elapsed, med_ms, probe_ms, launches = time_steps(tr, batch, args.steps, args.warmup, world,
-                                                     probe=dom)
+                                                     probe=dom, probe_every=args.probe_every)
     flags = tr.engine.device_errors()     # synchronises; after the timed region
     identical = None
     if world > 1:
@@ -731,7 +736,8 @@ def run_rank(args, world, rank, local):
            "step_tflops_algorithmic": round(step_tflops, 2),
            "ceiling": ceiling,
            "roofline": roof,
-           "probe": {"kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": launches},
+           "probe": {"kernel": dom, "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+                     "every": args.probe_every},
            "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()}}
 
     rc = health(out, flags, identical)

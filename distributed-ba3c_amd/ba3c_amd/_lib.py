@@ -91,6 +91,7 @@ def load():
         "ba3c_sample": (i32, [P, P, P, i32, i32, P, P]),
         "ba3c_greedy": (i32, [P, P, P, P, i32, i32, ctypes.c_double, P]),
         "ba3c_probe_enable": (i32, [P, i32]),
+        "ba3c_probe_every": (i32, [P, i32]),
         "ba3c_probe_read": (i32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]),
         "ba3c_device_errors": (i32, [P, ctypes.POINTER(ctypes.c_uint32)]),
         "ba3c_kernel_split": (i32, [P, i32]),

@@ -246,9 +246,12 @@ class Ba3cEngine(object):
         return actions
 
     # -- timing probe -------------------------------------------------------------------
-    def probe_enable(self, kernel):
+    def probe_enable(self, kernel, every=1):
+        """Bracket launches of `kernel` (None: stop) with HIP events, the first of every
+        `every` of them (ba3c_probe_every)."""
         kid = -1 if kernel is None else _lib.KERNEL_IDS[kernel]
         _lib.check(self.lib.ba3c_probe_enable(self.h, kid))
+        _lib.check(self.lib.ba3c_probe_every(self.h, int(every)))
 
     def kernel_merged(self, kernel):
         """Kernel names that ran inside `kernel`'s launch in the last training pass (multi-job

@@ -199,6 +199,8 @@ struct ba3c_handle {
   int probe_kernel = -1;
   std::vector<hipEvent_t> ev_begin, ev_end;
   int probe_used = 0;
+  int probe_every = 1;        // ba3c_probe_every: bracket one launch in `probe_every`
+  unsigned probe_seen = 0;    // launches of probe_kernel since ba3c_probe_enable
   int probe_launches = 0;
   double probe_ms = 0.0;
 };
@@ -418,7 +420,8 @@ struct ProbeScope {
   hipStream_t s;
   bool on;
   ProbeScope(ba3c_handle* h_, hipStream_t s_, int kid) : h(h_), s(s_), on(false) {
-    if (h->probe_kernel == kid && h->probe_used < (int)h->ev_begin.size()) {
+    if (h->probe_kernel == kid && h->probe_seen++ % (unsigned)h->probe_every == 0 &&
+        h->probe_used < (int)h->ev_begin.size()) {
       on = true;
       (void)hipEventRecord(h->ev_begin[h->probe_used], s);
     }
@@ -1845,6 +1848,7 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id) {
     }
   }
   h->probe_kernel = kernel_id;
+  h->probe_seen = 0;
   h->probe_used = 0;
   h->probe_ms = 0.0;
   h->probe_launches = 0;
@@ -2042,6 +2046,14 @@ int ba3c_allreduce_mean(ba3c_handle* h, void* stream, float* grads, int64_t coun
   hipLaunchKernelGGL(scale_kernel, dim3((unsigned)std::min<int64_t>((count + 1023) / 1024, 4096)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), grads, count, inv);
   HIP_TRY(hipGetLastError());
+  return BA3C_OK;
+}
+
+int ba3c_probe_every(ba3c_handle* h, int32_t n) {
+  if (!h) return fail(BA3C_ERR_INVALID, "null handle");
+  if (n < 1) return fail(BA3C_ERR_INVALID, "probe interval must be >= 1");
+  h->probe_every = n;
+  h->probe_seen = 0;
   return BA3C_OK;
 }
 

@@ -242,6 +242,10 @@ int ba3c_probe_enable(ba3c_handle* h, int32_t kernel_id);
 int ba3c_device_errors(ba3c_handle* h, uint32_t* flags);
 
 int ba3c_probe_read(ba3c_handle* h, double* total_ms, int32_t* launches);
+/* Bracket only the first of every `n` launches of the probed kernel (default 1: every launch),
+ * counted from here / from ba3c_probe_enable.  Each bracket's two events leave 5-6 us gaps in
+ * the stream, so a throughput run samples its launches (bench.py --probe-every). */
+int ba3c_probe_every(ba3c_handle* h, int32_t n);
 /* The synchronous gradient exchange through the C ABI (SURVEY.md §8b `ba3c_allreduce_mean`;
  * replaces the SyncReplicasOptimizer aggregation on the parameter servers,
  * OpenAIGym/train.py:598-606): an RCCL communicator owned by the handle.  RCCL is resolved at

@@ -267,3 +267,28 @@ def test_cabi_rccl_exchange_world1():
     _lib.check(lib.ba3c_comm_unique_id(uid))
     _lib.check(lib.ba3c_comm_init(eng.h, uid, 1, 0))
     _lib.check(lib.ba3c_comm_destroy(eng.h, 1))
+
+
+def test_probe_every_brackets_one_launch_in_n():
+    """ba3c_probe_every (bench.py --probe-every): the probe brackets the first of every n
+    launches of its kernel from ba3c_probe_enable on; probe_enable(None) restores n = 1."""
+    B = 32
+    cfgk = dict(A=4, C=4, F=128, S=4)
+    params, state, action, R, cfg = case(77, B, **cfgk)
+    eng = engine(max_batch=B, **cfgk)
+    eng.load_params(params)
+    args = (dev(state), dev(action), dev(R))
+    for every, steps, want in ((1, 4, 4), (3, 7, 3), (5, 5, 1)):
+        eng.probe_enable("conv1_fwd", every)
+        for _ in range(steps):
+            eng.train_grads(*args)
+        ms, n = eng.probe_read()
+        assert n == want and ms > 0, (every, steps, n, ms)
+    eng.probe_enable(None)
+    with pytest.raises(RuntimeError):
+        _lib_check_every(eng, 0)
+
+
+def _lib_check_every(eng, n):
+    from ba3c_amd import _lib
+    _lib.check(eng.lib.ba3c_probe_every(eng.h, n))
