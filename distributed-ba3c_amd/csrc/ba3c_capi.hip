@@ -312,7 +312,7 @@ struct WgradPlan {
   int M, N, K, S, kchunk, mt, nt;
 };
 
-WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN) {
+WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN, int target = kWgradTargetBlocks) {
   WgradPlan w;
   w.M = M;
   w.N = N;
@@ -320,12 +320,32 @@ WgradPlan plan_wgrad(int M, int N, int K, int BM, int BN) {
   w.mt = (M + BM - 1) / BM;
   w.nt = (N + BN - 1) / BN;
   const int ktiles = (K + GEMM_BK - 1) / GEMM_BK;
-  int S = (kWgradTargetBlocks + w.mt * w.nt - 1) / (w.mt * w.nt);
+  int S = (target + w.mt * w.nt - 1) / (w.mt * w.nt);
   S = std::max(1, std::min(S, (ktiles + 3) / 4));   // >= 4 k-tiles per split
   const int tiles_per = (ktiles + S - 1) / S;
   w.kchunk = tiles_per * GEMM_BK;
   w.S = (K + w.kchunk - 1) / w.kchunk;
   return w;
+}
+
+// fc1's backward at large batches (the multi-job launch): 128 x 128 tiles for the input and
+// weight gradients instead of 64 x 64 / 128 x 64.  The engine splits every staged fp32 value
+// into three bf16 planes (ba3c_gemm6.h), and at the small tiles that staging issued 10.8 VALU
+// instructions per MFMA (PMC): four times the MFMAs per staged value.  The weight gradient
+// takes fewer, longer K slabs (BA3C_FC1W_TARGET workgroups: 5 slabs at B = 2048, F = 512).
+// Measured (r06v, r06w): the launch 0.0600 -> 0.0586 ms and the all-layer reduction 29.2 ->
+// 28.0 us (half the fc1 slabs); not the 3x the VALU count suggested — the two workgroups per CU
+// that 60 KB of LDS allows leave each k-tile's staging exposed, and 3- / 4-deep load rings
+// (BA3C_FCD_DEPTH) made it 0.079 / 0.080 ms.
+#ifndef BA3C_FC1_BIGTILE
+#define BA3C_FC1_BIGTILE 1
+#endif
+#ifndef BA3C_FC1W_TARGET
+#define BA3C_FC1W_TARGET 256
+#endif
+WgradPlan fc1w_plan(int F, int B, bool legacy, bool bigtile) {
+  return bigtile ? plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 128, BA3C_FC1W_TARGET)
+                 : plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
 }
 
 // geometry constants (train.py:92, :177-212)
@@ -358,7 +378,8 @@ PartialSizes partial_sizes(const ba3c_handle* h, int B) {
   auto sz = [](const WgradPlan& w) { return (size_t)w.S * w.M * w.N; };
   PartialSizes p;
   p.heads = sz(plan_wgrad(F + 1, h->cfg.num_actions + 1, B, 128, 32));
-  p.fc1 = sz(plan_wgrad(1600 + (h->cfg.replace_with_conv ? 0 : 1), F, B, 128, 64));
+  const bool legacy = !h->cfg.replace_with_conv;
+  p.fc1 = std::max(sz(fc1w_plan(F, B, legacy, false)), sz(fc1w_plan(F, B, legacy, true)));
   p.conv3 = std::max(sz(plan_wgrad(576, 64, B * 25, 128, 64)), (size_t)C3W_P * 576 * 64);
   p.conv2 = std::max(sz(plan_wgrad(800, 64, B * 196, 128, 64)), (size_t)W6_P2 * Lay::W2::M * Lay::W2::COUT);
   p.conv1 = std::max(sz(plan_wgrad(800, 32, B * 1296, 128, 32)), (size_t)WG_P1 * Lay::W1::M * Lay::W1::COUT);
@@ -798,6 +819,13 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
                          dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, 4>), grid, dim3(GEMM_THREADS), 0, s, fc);
+#ifndef BA3C_FC1F_BIGTILE
+#define BA3C_FC1F_BIGTILE 0   // full grids on 128 x 128 tiles (same K chunks: bit-identical; r06v
+                              // 0.0299 -> 0.0333 ms, not used)
+#endif
+    else if (h->g6 && BA3C_FC1F_BIGTILE)
+      hipLaunchKernelGGL((gemm6_kernel<128, 128, 2, 2, FcFwd, BA3C_FC_DEPTH>), dim3(grid.x, (F + 127) / 128, grid.z),
+                         dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6)
       hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, BA3C_FC_DEPTH>), grid, dim3(GEMM_THREADS), 0, s, fc);
     else
@@ -858,6 +886,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   static_assert(OVERLAP_B <= SMALL_B, "multi-job conv2 input gradient is the small-batch geometry");
   if (!mj && h->side && (h->overlap == 1 || B <= OVERLAP_B)) ws = h->side;
   const bool big = B > OVERLAP_B;   // multi-job gemm jobs: 2-deep k-tile rings (full grids)
+  const bool fc1big = BA3C_FC1_BIGTILE && mj_fc && big;   // fc1w_plan
   // every weight-gradient reduction is deferred into one launch at the end (RAII: an early
   // error return leaves the handle in immediate mode)
   struct DeferGuard {
@@ -906,11 +935,12 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   {
     WgradPlan pl = plan_wgrad(F + 1, A + 1, B, 128, 32);
     BatchWgrad g{w.h, w.dzv, w.part_h, F, MAXA, 1, pl.M, pl.N, pl.K, pl.kchunk};
-    WgradPlan plf = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
+    WgradPlan plf = fc1w_plan(F, B, legacy, fc1big);
     BatchWgrad gf{w.a3, w.dh, w.part_f, 1600, F, legacy ? 1 : 0, plf.M, plf.N, plf.K, plf.kchunk};
     FcDgrad d{w.dh, Wfc, w.a3, w.dy3, h->per, h->wstride, B, 1600, F, 0};
-    const dim3 gd((d.M + 63) / 64, (d.N + 63) / 64, 1), gh((pl.M + 127) / 128, (pl.N + 31) / 32, pl.S),
-        gff((plf.M + 127) / 128, (plf.N + 63) / 64, plf.S);
+    const int dbm = fc1big ? 128 : 64, fbn = fc1big ? 128 : 64;
+    const dim3 gd((d.M + dbm - 1) / dbm, (d.N + dbm - 1) / dbm, 1), gh((pl.M + 127) / 128, (pl.N + 31) / 32, pl.S),
+        gff((plf.M + 127) / 128, (plf.N + fbn - 1) / fbn, plf.S);
     if (mj_fc)   // fc1 input gradient + head and fc1 weight gradients: one launch
       h->merged[BA3C_K_FC1_DGRAD] |= (1u << BA3C_K_FC1_WGRAD) | (1u << BA3C_K_HEAD_WGRAD);
     if (mj_fc && !big)
@@ -919,6 +949,11 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
 #ifndef BA3C_FCD_DEPTH
 #define BA3C_FCD_DEPTH 2      // k-tile ring depth of the large-batch fc1 backward jobs (A/B)
 #endif
+    else if (mj_fc && fc1big)
+      CHECK((launch_multi<false, Gemm6Job<128, 128, 2, 2, FcDgrad, BA3C_FCD_DEPTH>,
+                          Gemm6Job<128, 32, 4, 1, BatchWgrad, BA3C_FCD_DEPTH>,
+                          Gemm6Job<128, 128, 2, 2, BatchWgrad, BA3C_FCD_DEPTH>>(s, d, gd, g, gh, gf, gff, h,
+                                                                              BA3C_K_FC1_DGRAD)));
     else if (mj_fc)
       CHECK((launch_multi<false, Gemm6Job<64, 64, 2, 2, FcDgrad, BA3C_FCD_DEPTH>, Gemm6Job<128, 32, 4, 1, BatchWgrad, BA3C_FCD_DEPTH>,
                           Gemm6Job<128, 64, 2, 2, BatchWgrad, BA3C_FCD_DEPTH>>(s, d, gd, g, gh, gf, gff, h, BA3C_K_FC1_DGRAD)));
@@ -937,7 +972,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
   }
   // fc1 weight (+ legacy bias) gradient
   {
-    WgradPlan pl = plan_wgrad(1600 + (legacy ? 1 : 0), F, B, 128, 64);
+    WgradPlan pl = fc1w_plan(F, B, legacy, fc1big);
     BatchWgrad g{w.a3, w.dh, w.part_f, 1600, F, legacy ? 1 : 0, pl.M, pl.N, pl.K, pl.kchunk};
     if (!mj_fc) CHECK((launch_gemm<128, 64, 2, 2>(h, ws, BA3C_K_FC1_WGRAD, g, pl.S)));
     ReduceMap mp{};
