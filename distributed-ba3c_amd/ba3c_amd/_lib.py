@@ -39,7 +39,7 @@ class Ba3cOptParams(ctypes.Structure):
 
 _lib = None
 # roofline-accounting queries an alternative A/B build (BA3C_LIB) may predate
-AB_OPTIONAL = {"ba3c_kernel_merged"}
+AB_OPTIONAL = {"ba3c_kernel_merged", "ba3c_probe_every"}
 
 
 def load():

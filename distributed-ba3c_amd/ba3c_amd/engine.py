@@ -251,7 +251,8 @@ class Ba3cEngine(object):
         `every` of them (ba3c_probe_every)."""
         kid = -1 if kernel is None else _lib.KERNEL_IDS[kernel]
         _lib.check(self.lib.ba3c_probe_enable(self.h, kid))
-        _lib.check(self.lib.ba3c_probe_every(self.h, int(every)))
+        if every != 1 or hasattr(self.lib, "ba3c_probe_every"):   # (A/B builds predating it)
+            _lib.check(self.lib.ba3c_probe_every(self.h, int(every)))
 
     def kernel_merged(self, kernel):
         """Kernel names that ran inside `kernel`'s launch in the last training pass (multi-job
