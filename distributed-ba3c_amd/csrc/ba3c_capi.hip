@@ -732,9 +732,13 @@ int launch_conv0_band(ba3c_handle* h, hipStream_t s, const BandArgs& a, const Wo
 
 // conv3 forward / input gradient: persistent whole-image workgroups, two per CU (ba3c_conv3.h)
 template <bool DG>
+#ifndef BA3C_C3_WGPC
+#define BA3C_C3_WGPC 2   // conv3's whole-image kernels: persistent workgroups per CU (r06z: 1 made
+                         // the forward 19.8 -> 23.9 us and the input gradient 29.3 -> 33.8 us)
+#endif
 int launch_conv3(ba3c_handle* h, hipStream_t s, int kid, const Conv3Args& a) {
   if (a.batch <= 0) return BA3C_OK;
-  const dim3 grid(std::min(a.batch, 2 * h->cus));
+  const dim3 grid(std::min(a.batch, BA3C_C3_WGPC * h->cus));
   {
     ProbeScope ps(h, s, kid);
     hipLaunchKernelGGL(conv3_band_kernel<DG>, grid, dim3(256), 0, s, a);
@@ -1029,7 +1033,7 @@ int run_backward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t*
         h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_CONV3_WGRAD;
       } else {
         if (big && h->pend_scalars) {
-          CHECK((launch_multi<true, Conv3DJob, ScalarsJob>(s, da, dim3(std::min(B, 2 * h->cus)), h->scalars_args,
+          CHECK((launch_multi<true, Conv3DJob, ScalarsJob>(s, da, dim3(std::min(B, BA3C_C3_WGPC * h->cus)), h->scalars_args,
                                                             dim3(1), 0, dim3(0, 1, 1), h, BA3C_K_CONV3_DGRAD)));
           h->merged[BA3C_K_CONV3_DGRAD] |= 1u << BA3C_K_SCALARS;   // the reduction rode on this launch
           h->pend_scalars = false;
