@@ -350,10 +350,19 @@ WgradPlan fc1w_plan(int F, int B, bool legacy, bool bigtile) {
 
 // geometry constants (train.py:92, :177-212)
 constexpr int P0 = 40 * 40 * 32, P1 = 18 * 18 * 32, P2 = 7 * 7 * 64, A3 = 1600;
-// FC1 fwd split-K: 10 fixed chunks of 5 k-tiles (batch-independent rounding).  r02: 416 (4
-// chunks of 13 k-tiles) left B=32 with 8 workgroups walking 13 dependent k-tiles (17.6 us)
+// FC1 fwd split-K: 5 fixed chunks of 10 k-tiles (batch-independent rounding), each the sum
+// of its even and its odd k-tiles (BA3C_FC_HALVES, gemm6_body PAR: two groups at B <= 64, one
+// group with two accumulator sets above; the same association, so every row rounds the same
+// at any batch).
+// r02: 416 (4 chunks of 13 k-tiles) left B=32 with 8 workgroups walking 13 dependent k-tiles
+// (17.6 us).  r06aa / r06ab: 5 chunks instead of 10 (half the partial sums written by fc1 and
+// read by the heads kernel) took the B=2048 step 1.713 -> 1.685 and 1.685 -> 1.665 ms, but
+// B=32 0.1565 -> 0.1612 ms with 10 k-tiles per workgroup in series: hence the two groups.
+#ifndef BA3C_FC_HALVES
+#define BA3C_FC_HALVES 1
+#endif
 #ifndef BA3C_FC_KCHUNK
-#define BA3C_FC_KCHUNK 160
+#define BA3C_FC_KCHUNK (BA3C_FC_HALVES ? 320 : 160)
 #endif
 constexpr int FC_KCHUNK = BA3C_FC_KCHUNK, FC_SPLIT = (A3 + FC_KCHUNK - 1) / FC_KCHUNK;
 static_assert(FC_SPLIT <= FC_SPLIT_MAX, "heads kernel finishes at most FC_SPLIT_MAX chunks");
@@ -408,7 +417,10 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
   w.p2 = (float*)take(Bz * P2 * 4);
   w.a3 = (float*)take(Bz * A3 * 4);
   w.h = (float*)take(Bz * F * 4);
-  w.fcpart = (float*)take((size_t)FC_SPLIT * Bz * F * 4);
+#ifndef BA3C_FCPART_LAST
+#define BA3C_FCPART_LAST 0   // A/B: fc1's forward partials at the end of the workspace
+#endif
+  if (!BA3C_FCPART_LAST) w.fcpart = (float*)take((size_t)FC_SPLIT * Bz * F * 4);
   w.relu = (unsigned long long*)take(RELU_WORDS * 8);
   w.wt = (float*)take((size_t)WT_TOTAL * 4);
   w.wt6 = (uint16_t*)take((size_t)3 * WT_C0F * 2);
@@ -431,6 +443,7 @@ Workspace carve(const ba3c_handle* h, void* base, int B, bool train) {
     w.part_1 = (float*)take(ps.conv1 * 4);
     w.part0 = (float*)take(max_partials0(h, B) * 4);
   }
+  if (BA3C_FCPART_LAST) w.fcpart = (float*)take((size_t)FC_SPLIT * Bz * F * 4);
   w.bytes = off;
   return w;
 }
@@ -818,20 +831,22 @@ int run_forward(ba3c_handle* h, hipStream_t s, const float* prm, const uint8_t* 
   {
     ProbeScope ps(h, s, BA3C_K_FC1_FWD);
     const dim3 grid((B + 127) / 128, (F + 63) / 64, FC_SPLIT);
+    constexpr bool HV = BA3C_FC_HALVES;
+    constexpr int KSS = HV ? 2 : 1;   // small batches: even and odd k-tiles in two groups
     if (h->g6 && B <= 64)   // 64-row tiles: same per-row K order, half the dead rows staged
-      hipLaunchKernelGGL((gemm6_kernel<64, 64, 2, 2, FcFwd, 4>), dim3((B + 63) / 64, grid.y, grid.z),
-                         dim3(GEMM_THREADS), 0, s, fc);
+      hipLaunchKernelGGL((gemm6_kernel<64, 64, 2, 2, FcFwd, 4, KSS, HV>), dim3((B + 63) / 64, grid.y, grid.z),
+                         dim3(GEMM_THREADS * KSS), 0, s, fc);
     else if (h->g6 && (int)(grid.x * grid.y * grid.z) < h->cus)
-      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, 4>), grid, dim3(GEMM_THREADS), 0, s, fc);
+      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, 4, 1, HV>), grid, dim3(GEMM_THREADS), 0, s, fc);
 #ifndef BA3C_FC1F_BIGTILE
 #define BA3C_FC1F_BIGTILE 0   // full grids on 128 x 128 tiles (same K chunks: bit-identical; r06v
                               // 0.0299 -> 0.0333 ms, not used)
 #endif
     else if (h->g6 && BA3C_FC1F_BIGTILE)
-      hipLaunchKernelGGL((gemm6_kernel<128, 128, 2, 2, FcFwd, BA3C_FC_DEPTH>), dim3(grid.x, (F + 127) / 128, grid.z),
+      hipLaunchKernelGGL((gemm6_kernel<128, 128, 2, 2, FcFwd, BA3C_FC_DEPTH, 1, HV>), dim3(grid.x, (F + 127) / 128, grid.z),
                          dim3(GEMM_THREADS), 0, s, fc);
     else if (h->g6)
-      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, BA3C_FC_DEPTH>), grid, dim3(GEMM_THREADS), 0, s, fc);
+      hipLaunchKernelGGL((gemm6_kernel<128, 64, 2, 2, FcFwd, BA3C_FC_DEPTH, 1, HV>), grid, dim3(GEMM_THREADS), 0, s, fc);
     else
       hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, FcFwd>), grid, dim3(GEMM_THREADS), 0, s, fc);
   }

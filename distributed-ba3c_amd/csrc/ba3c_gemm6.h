@@ -51,10 +51,17 @@ struct Gemm6Lds {
 // first ceil(n/2), group 1 the rest, each with its own staging LDS and the same trip count),
 // and group 0 adds group 1's accumulators (acc0 + acc1) before the epilogue.  Small launches
 // (a few workgroups walking a long K) run their serial k-tile chain at half the length.
-template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2, int KS = 1>
+// PAR: the k-tiles split by parity instead of in halves — KS = 2: group g takes tiles g, g + 2,
+// ...; KS = 1: even tiles into one accumulator set and odd ones into a second (compile-time:
+// G6_DEPTH is even), added at the end.  Both forms compute (sum of even tiles) + (sum of odd
+// tiles) with the same order inside each sum, so a problem can run two groups at small batches
+// and one at large ones with every output rounded the same.
+template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2, int KS = 1, bool PAR = false>
 __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, char* lds) {
   static_assert(WGM * WGN == 4, "4 waves per group");
   static_assert(KS == 1 || KS == 2, "k groups");
+  static_assert(!PAR || G6_DEPTH % 2 == 0, "parity sets need an even ring depth");
+  constexpr int NSET = PAR && KS == 1 ? 2 : 1;
   constexpr int BK = GEMM_BK;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -85,7 +92,13 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
   // k-tiles of this group; both groups run the same trip count (a tile past the group's
   // kend reads the zero block)
   int ntiles = (kend - kbeg + BK - 1) / BK;
-  if constexpr (KS == 2) {
+  // k offset of this group's i-th tile (PAR, KS = 2: tile 2 i + grp; past kend: the zero block)
+  int kstep = BK;
+  if constexpr (KS == 2 && PAR) {
+    ntiles = (ntiles + 1) / 2;
+    kbeg += grp * BK;
+    kstep = 2 * BK;
+  } else if constexpr (KS == 2) {
     ntiles = (ntiles + 1) / 2;
     kbeg += grp * ntiles * BK;
     kend = min(kend, kbeg + ntiles * BK);
@@ -163,13 +176,16 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
     }
   };
 
-  f32x16 acc[TM][TN];
+  f32x16 accs[NSET][TM][TN];
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+  for (int q = 0; q < NSET; ++q)
 #pragma unroll
-    for (int b = 0; b < TN; ++b)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accs[q][a][b][r] = 0.f;
+  f32x16 (&acc)[TM][TN] = accs[0];
 
   const int li = lane & 31, lh = lane >> 5;
   // fragment base of this lane: row reads at [row li][K 8 lh]; transposed reads: lane 4q + p
@@ -189,7 +205,7 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
     return __builtin_bit_cast(bf16x8v, u32x4{u0.x, u0.y, u1.x, u1.y});
   };
 
-  auto tile = [&](int k0) {
+  auto tile = [&](int k0, f32x16 (&ac)[TM][TN]) {
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8v av[3][TM], bv[3][TN];
@@ -208,7 +224,7 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
         for (int a = 0; a < TM; ++a)
 #pragma unroll
           for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[PA_[pr]][a], bv[PB_[pr]][b], acc[a][b], 0, 0, 0);
+            ac[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[PA_[pr]][a], bv[PB_[pr]][b], ac[a][b], 0, 0, 0);
     }
   };
 
@@ -218,19 +234,19 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
   // G6_DEPTH tiles (the last may be partial: its loads mask k >= kend) run branch-free; the
   // < G6_DEPTH tail tiles are already in the ring.
 #pragma unroll
-  for (int st = 0; st < G6_DEPTH - 1; ++st) load(st, kbeg + st * BK);
+  for (int st = 0; st < G6_DEPTH - 1; ++st) load(st, kbeg + st * kstep);
   int it = 0;
   for (; it + G6_DEPTH - 1 < ntiles; it += G6_DEPTH) {   // >= G6_DEPTH tiles left
-    const int kk = kbeg + it * BK;
+    const int kk = kbeg + it * kstep;
 #pragma unroll
     for (int st = 0; st < G6_DEPTH; ++st) {
       // sched barriers: the split arithmetic of a later stage would otherwise be hoisted to
       // the top of the group, waiting for loads that are meant to stay in flight
       __builtin_amdgcn_sched_barrier(0);
-      load((st + G6_DEPTH - 1) % G6_DEPTH, kk + (st + G6_DEPTH - 1) * BK);
+      load((st + G6_DEPTH - 1) % G6_DEPTH, kk + (st + G6_DEPTH - 1) * kstep);
       store(st);
       __syncthreads();
-      tile(kk + st * BK);
+      tile(kk + st * kstep, accs[st % NSET]);   // (it is a multiple of the even depth)
       __syncthreads();
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -240,9 +256,17 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
     if (it + st < ntiles) {                    // uniform
       store(st);
       __syncthreads();
-      tile(kbeg + (it + st) * BK);
+      tile(kbeg + (it + st) * kstep, accs[st % NSET]);
       __syncthreads();
     }
+  }
+  if constexpr (NSET == 2) {                   // (even tiles) + (odd tiles)
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = accs[0][a][b][r] + accs[1][a][b][r];
   }
 
   if constexpr (KS == 2) {
@@ -270,10 +294,10 @@ __device__ __forceinline__ void gemm6_body(const P& p, int bx, int by, int bz, c
   p.template epilogue<TM, TN>(acc, m0 + wm * WTM, n0 + wn * WTN, lane, bz);
 }
 
-template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2, int KS = 1>
+template <int BM, int BN, int WGM, int WGN, class P, int G6_DEPTH = 2, int KS = 1, bool PAR = false>
 __global__ void __launch_bounds__(GEMM_THREADS * KS) gemm6_kernel(const P p) {
   __shared__ __attribute__((aligned(16))) char lds[KS * Gemm6Lds<BM, BN, P>::BYTES];
-  gemm6_body<BM, BN, WGM, WGN, P, G6_DEPTH, KS>(p, blockIdx.x, blockIdx.y, blockIdx.z, lds);
+  gemm6_body<BM, BN, WGM, WGN, P, G6_DEPTH, KS, PAR>(p, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
 }  // namespace ba3c
